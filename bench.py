@@ -1,0 +1,259 @@
+"""bench.py -- MC trial-moves/s of the checkerboard Metropolis hot path on MI355X.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--cps 128] [--atoms 10000000]
+  torchrun --nproc-per-node N bench.py --gpus N ...     (one rank per GPU, z-slab decomposition)
+
+A "step" is one full MC sweep (8 checkerboard colour phases + shiftCells) of BASELINE.json
+config 3 (128^3 cells, 1e7 particles per GPU, w=rc=2.5, beta=0.3, sigma=0.5, n_M=10, nmax=16,
+Philox seed 1234, reference lattice start) with the state resident in HBM.  With N>1 ranks every
+rank owns a 128^3-cell slab of a 128x128x(128N) periodic box (weak scaling; the 8-rank point has
+the per-GPU work of config 5) and exchanges halo planes with its z-neighbours over RCCL.
+
+Rank 0 prints ONE JSON line with value = trial moves per second over all ranks, the roofline of
+the dominant kernel (subsweep; algorithmic bytes per launch / HIP-event launch time vs 8 TB/s)
+and the CPU baseline (the C oracle, OpenMP over the cells of a colour, on a bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "parallel-monte-carlo_amd"))
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def stencil_counts(n: np.ndarray, cps: tuple[int, int, int]) -> np.ndarray:
+    """S_c = particles in the 27-cell periodic stencil of every cell (whole box)."""
+    cx, cy, cz = cps
+    g = n.reshape(cz, cy, cx).astype(np.int64)
+    s = np.zeros_like(g)
+    for dz in (-1, 0, 1):
+        for dy in (-1, 0, 1):
+            for dx in (-1, 0, 1):
+                s += np.roll(g, shift=(-dz, -dy, -dx), axis=(0, 1, 2))
+    return s.reshape(-1)
+
+
+def algorithmic_bytes_per_sweep(n_owned: np.ndarray, stencil: np.ndarray) -> dict:
+    """SURVEY.md 8(d) staged model: per visited (non-empty) cell read its 27-cell stencil
+    (12 B per particle), 27 counts (2 B each) and write its own particles (12 B each)."""
+    ne = n_owned > 0
+    sub = float(np.sum(12 * stencil[ne] + 54 + 12 * n_owned[ne]))
+    shift = float(np.sum(36 * n_owned.astype(np.int64) + 6)) * 1.0
+    return {"subsweep_sweep": sub, "subsweep_launch": sub / 8.0, "shift": shift}
+
+
+def cpu_baseline(disk: np.ndarray, n: np.ndarray, cps: int, sweeps: int, threads: int, sweep0: int) -> dict:
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pmc_oracle  # test infrastructure: timed CPU baseline only
+    pmc_oracle.build()
+    st = pmc_oracle.OracleState(pmc_oracle.make_params(cps=cps))
+    st.disk[:] = disk
+    st.n[:] = n
+    pmc_oracle.set_threads(threads)
+    t0 = time.perf_counter()
+    st.run(sweep0, sweeps)
+    dt = time.perf_counter() - t0
+    trials = st.stats.trials
+    return {"value": trials / dt, "unit": "trial-moves/s", "cores": threads, "kind": "port",
+            "sample": f"{sweeps} full sweep(s) of the {cps}^3-cell box from the GPU state "
+                      f"(C oracle, OpenMP over cells of a colour, {threads} threads), {dt:.2f} s"}
+
+
+def traffic_from_profile() -> dict | None:
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except Exception:
+        return None
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--cps", type=int, default=128)
+    ap.add_argument("--atoms", type=int, default=10_000_000)
+    ap.add_argument("--cpu-sweeps", type=int, default=1)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--graph", action="store_true", help="replay the timed sweeps as one hipGraph")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import pmc_amd
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    stream = torch.cuda.Stream()
+    cps = args.cps
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    if world == 1:
+        sim = pmc_amd.PmcContext(cps, stream=stream.cuda_stream)
+        sim.init_lattice(args.atoms)
+        run_phase = sim.phase
+        run_shift = sim.shift
+        halo_after_phase = lambda colour: None  # noqa: E731
+        halo_after_shift = lambda: None  # noqa: E731
+        cps_z = cps
+    else:
+        from pmc_amd.slab import SlabSimulation
+        sim_s = SlabSimulation.create(cps=cps, nz_local=cps, rank=rank, world=world, stream=stream,
+                                      atoms_per_rank=args.atoms)
+        sim = sim_s.ctx
+        run_phase = sim_s.phase_only
+        run_shift = sim_s.shift_only
+        halo_after_phase = sim_s.exchange_after_phase
+        halo_after_shift = sim_s.exchange_after_shift
+        cps_z = cps * world
+
+    plan_cache = {}
+
+    def plan(s):
+        if s not in plan_cache:
+            sys.path.insert(0, os.path.join(REPO, "parallel-monte-carlo_amd"))
+            from pmc_amd.plan import sweep_plan
+            plan_cache[s] = sweep_plan(1234, s, 2.5)
+        return plan_cache[s]
+
+    events = []
+
+    def one_sweep(s, record):
+        order, _, _ = plan(s)
+        for colour in order:
+            if record:
+                a = torch.cuda.Event(enable_timing=True)
+                b = torch.cuda.Event(enable_timing=True)
+                a.record(stream)
+            run_phase(colour, s)
+            if record:
+                b.record(stream)
+                events.append((a, b))
+            halo_after_phase(colour)
+        run_shift(s)
+        halo_after_shift()
+
+    # warmup
+    for s in range(args.warmup):
+        one_sweep(s, False)
+    torch.cuda.synchronize()
+    sim.stats(reset=True)
+    # algorithmic bytes from the state at the start of the timed region
+    disk_h, n_h = sim.copy_out()
+    plane = cps * cps
+    lo = plane if world > 1 else 0
+    n_owned = n_h[lo:lo + plane * cps].astype(np.int64)
+    if world == 1:
+        stencil = stencil_counts(n_owned, (cps, cps, cps))
+    else:
+        ext = n_h.astype(np.int64).reshape(cps + 2, cps, cps)
+        g = ext
+        s = np.zeros((cps, cps, cps), np.int64)
+        for dz in (-1, 0, 1):
+            sub = g[1 + dz:1 + dz + cps]
+            for dy in (-1, 0, 1):
+                for dx in (-1, 0, 1):
+                    s += np.roll(sub, shift=(-dy, -dx), axis=(1, 2))
+        stencil = s.reshape(-1)
+    abytes = algorithmic_bytes_per_sweep(n_owned, stencil)
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    first = args.warmup
+    if args.graph and world == 1:
+        sim.run_graph(first, args.steps)
+    else:
+        for k in range(args.steps):
+            one_sweep(first + k, True)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    st = sim.stats()
+    trials_local = st["trials"]
+    phase_ms = [a.elapsed_time(b) for a, b in events] if events else []
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        tr = torch.tensor([trials_local], dtype=torch.int64, device="cuda")
+        dist.all_reduce(tr)
+        trials_total = int(tr.item())
+    else:
+        trials_total = trials_local
+    flags = sim.error_flags()
+    value = trials_total / elapsed
+
+    if rank == 0:
+        avg_launch_s = (float(np.mean(phase_ms)) * 1e-3) if phase_ms else None
+        achieved = (abytes["subsweep_launch"] / avg_launch_s / 1e9) if avg_launch_s else None
+        traffic = traffic_from_profile()
+        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                "traffic": traffic.get("subsweep_bytes_per_launch") if traffic else None,
+                "kernel": "k_subsweep<16> (one colour phase)",
+                "launch_ms": avg_launch_s * 1e3 if avg_launch_s else None,
+                "algorithmic_bytes_per_launch": abytes["subsweep_launch"]}
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            try:
+                thr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+                cpu = cpu_baseline(disk_h, n_h, cps, args.cpu_sweeps, thr, first)
+            except Exception as e:  # the baseline is reported, never the measured value
+                cpu = {"error": repr(e)}
+        sweeps_per_s = args.steps / elapsed
+        out = {
+            "metric": "MC trial-moves/s (whole node)",
+            "value": value,
+            "unit": "trial-moves/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (reference simple-cubic lattice start, Philox seed 1234)",
+            "config": {"workload": f"{cps}^3 cells x {args.atoms:.0e} particles per GPU, full checkerboard "
+                                   f"sweep (8 colour phases + shiftCells), box {cps}x{cps}x{cps_z}",
+                       "cells_per_gpu": cps ** 3, "particles_per_gpu": args.atoms, "n_moves": 10,
+                       "nmax": 16, "beta": 0.3, "sigma": 0.5, "w": 2.5,
+                       "parallelism": f"z-slab x{world}" if world > 1 else "single GPU"},
+            "sweeps_per_s": sweeps_per_s,
+            "acceptance": st["accepted"] / st["trials"] if st["trials"] else None,
+            "error_flags": flags,
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,167 @@
+/*
+ * pmc.h -- C ABI of the MI355X-native checkerboard Monte Carlo hot path.
+ *
+ * Drop-in boundary for qingye3/parallel-monte-carlo (reference at /root/reference, read-only).
+ * The reference has no library or FFI; its call surface is the three __global__ entry points
+ * plus the `start` driver, all sharing the `disk`/`n` layout:
+ *
+ *   disk : float[cells][3][nmax]  -- cell c at c*3*nmax: x[nmax], y[nmax], z[nmax]
+ *          (start.cu:188, indexing subsweep.h:20-24 / start.cu:291-300)
+ *   n    : int16_t[cells]         -- particles per cell (start.cu:187)
+ *   r    : float[3*N]             -- SoA positions x[N], y[N], z[N] (start.cu:186, :54-56)
+ *   cell index = x + y*CPS + z*CPS^2  (get_cell_index, subsweep.h:14-16)
+ *
+ * Every entry point below cites the reference symbol it replaces.  Device pointers are HIP
+ * device pointers in the reference layout.  All functions return PMC_OK (0) or a negative
+ * pmc_status; they never print and never exit (the reference printf's and continues,
+ * start.cu:213-216).  One host thread per context; all work is enqueued on the context's
+ * stream (default: a stream created by pmc_create, or the one given to pmc_set_stream).
+ */
+#ifndef PMC_H
+#define PMC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    PMC_OK = 0,
+    PMC_ERR_ARG = -1,        /* invalid argument / parameter combination */
+    PMC_ERR_HIP = -2,        /* HIP runtime error (see pmc_last_error) */
+    PMC_ERR_OVERFLOW = -3,   /* a cell would hold more than nmax particles (reference: unchecked,
+                                shiftCells.h:90,121 -- SURVEY Appendix B S3) */
+    PMC_ERR_RANGE = -4,      /* a particle lies outside the (local) box in pmc_assign */
+    PMC_ERR_NODEV = -5       /* no HIP device available */
+} pmc_status;
+
+/* Runtime parameters (the reference uses compile-time #defines, start.cu:14-24). */
+typedef struct pmc_params {
+    int32_t cps_x;      /* cells per side along x (cellsPerSide); even, >= 4 */
+    int32_t cps_y;      /* cells along y (0 -> cps_x); even, >= 4 */
+    int32_t cps_z;      /* GLOBAL cells along z (0 -> cps_x); even, >= 4 */
+    int32_t nz_local;   /* z-planes owned by this context (0 -> cps_z); even */
+    int32_t z0;         /* global z index of the first owned plane; even */
+    int32_t halo;       /* 0: storage holds the whole periodic box (nz_local == cps_z);
+                           1: slab mode, one halo plane below and above the owned planes */
+    int32_t nmax;       /* particle slots per cell (nmax), 1..64 */
+    int32_t n_moves;    /* trial moves per cell visit (n_M) */
+    float w;            /* cell width == LJ cutoff rc (w); box L = cps * w */
+    float beta;         /* inverse temperature (beta) */
+    float sigma;        /* Gaussian trial-move width (sigma) */
+    uint32_t reserved;
+    uint64_t seed;      /* Philox key; the reference seeds cuRAND with 1234 (subsweep.h:259) */
+} pmc_params;
+
+/* Observables accumulated by the subsweep kernels (reference: kernel.cu:228,413-415 --
+ * accept_counter and d_Eblocks; the reference never reports acceptance). */
+typedef struct pmc_stats {
+    int64_t de_fixed;   /* sum of accepted dE, fixed point 2^-32 energy units */
+    int64_t accepted;   /* accepted trial moves */
+    int64_t trials;     /* all trial moves, including out-of-cell rejections */
+    int64_t evaluated;  /* trial moves that passed out_of_bound and had energies evaluated */
+} pmc_stats;
+
+/* Result of pmc_start (the reference main prints the energy trace, kernel.cu:695). */
+typedef struct pmc_result {
+    pmc_stats stats;    /* totals over the run */
+    double e_initial;   /* total energy before the run (cell-list, pmc_energy) */
+    double e_final;     /* total energy after the run */
+    double seconds;     /* device time of the run (HIP events) */
+    int64_t sweeps;     /* MC sweeps executed */
+} pmc_result;
+
+typedef struct pmc_ctx pmc_ctx;
+
+/* ---- context ---------------------------------------------------------------------- */
+/* Allocate device state (disk/n ping-pong pair, stats slots) on the current HIP device.
+ * Replaces the cudaMalloc block of main (start.cu:197-205). */
+int pmc_create(const pmc_params* params, pmc_ctx** out);
+void pmc_destroy(pmc_ctx* ctx);
+/* Enqueue all further work on `stream` (a hipStream_t; NULL = the null stream). */
+int pmc_set_stream(pmc_ctx* ctx, void* stream);
+/* Use caller-owned device buffers as the context state instead of its own (e.g. torch
+ * tensors for RCCL halo exchange).  Each disk buffer holds storage_cells*3*nmax floats, each
+ * n buffer storage_cells int16; buffer 0 is the current state. */
+int pmc_attach_state(pmc_ctx* ctx, float* disk0, int16_t* n0, float* disk1, int16_t* n1);
+/* Current state buffers (device pointers, reference layout), storage geometry. */
+int pmc_state(pmc_ctx* ctx, float** disk, int16_t** n);
+int64_t pmc_storage_cells(const pmc_ctx* ctx);
+/* Last error message of this thread ("" if none). */
+const char* pmc_last_error(void);
+
+/* ---- reference kernels ------------------------------------------------------------- */
+/* init_r (start.cu:47-58; index<N guard of kernel.cu:78-89): simple-cubic lattice of
+ * n_atoms particles into d_r[3*n_atoms] (SoA), N_cube = ceil(cbrt(n_atoms)) computed
+ * exactly (fixes start.cu:208 truncation).  In slab mode the lattice fills the owned slab. */
+int pmc_init_r(pmc_ctx* ctx, int64_t n_atoms, float* d_r);
+/* assign (start.cu:87-146): bin d_r into d_disk/d_n with the reference's half-open rule
+ * lb < x <= ub, particles of a cell in ascending index order.  Returns PMC_ERR_OVERFLOW if a
+ * cell exceeds nmax, PMC_ERR_RANGE if a particle is outside the owned box. */
+int pmc_assign(pmc_ctx* ctx, const float* d_r, int64_t n_atoms, float* d_disk, int16_t* d_n);
+/* subsweep_kernel (subsweep.h:240-300): one checkerboard colour phase, offset = (ox,oy,oz)
+ * in {0,1}^3 (start.cu:241-245).  `sweep` is the RNG counter (sweep index). */
+int pmc_subsweep(pmc_ctx* ctx, float* d_disk, const int16_t* d_n, const int offset[3],
+                 uint32_t sweep);
+/* shiftCells (shiftCells.h:28-144; semantics of the fixed copy
+ * CUDA-Parallel-MC/CUDA-Parallel-MC/shiftCells.h:23-112): shift the cell grid along axis
+ * f by d and re-bin.  Double-buffered: reads (d_disk_in,d_n_in), writes (d_disk_out,d_n_out)
+ * (the reference's in-place update is only race-free inside one block, shiftCells.h:135-143). */
+int pmc_shift_cells(pmc_ctx* ctx, const float* d_disk_in, const int16_t* d_n_in,
+                    float* d_disk_out, int16_t* d_n_out, int f, float d);
+
+/* ---- driver (start.cu:169-272 main loop, kernel.cu:652-701) ------------------------- */
+/* Initialise the context state from a lattice of n_atoms particles (init_r + assign). */
+int pmc_init_lattice(pmc_ctx* ctx, int64_t n_atoms);
+/* One full MC sweep on the context state: colour order from the sweep plan, 8 subsweeps,
+ * shiftCells, buffer swap (start.cu:237-260).  Asynchronous. */
+int pmc_sweep(pmc_ctx* ctx, uint32_t sweep);
+/* One colour phase (colour id 0..7, itoa start.cu:153-157) / the sweep plan's shiftCells on the
+ * context state (any mode; the slab driver interleaves these with halo exchange). */
+int pmc_phase(pmc_ctx* ctx, int colour, uint32_t sweep);
+int pmc_shift(pmc_ctx* ctx, uint32_t sweep);
+/* The per-sweep plan every rank replicates (no broadcast): colour order (FY_Shuffle + itoa,
+ * start.cu:34-44,153-157, reseeded from time() in the reference) and the shift axis/distance
+ * (kernel.cu:683-684), all from the host Philox stream keyed by `seed`. */
+int pmc_sweep_plan(uint64_t seed, uint32_t sweep, float w, int order[8], int* f, float* d);
+/* mc_passes sweeps starting at sweep index `first_sweep` (the `start` driver). */
+int pmc_start(pmc_ctx* ctx, uint32_t first_sweep, int mc_passes, pmc_result* out);
+/* Record the sweep loop (pmc_sweep for sweeps first..first+count-1) as a hipGraph and
+ * replay it; identical results to calling pmc_sweep in a loop. */
+int pmc_run_graph(pmc_ctx* ctx, uint32_t first_sweep, int count);
+
+/* ---- observables ------------------------------------------------------------------- */
+/* Total LJ energy of the owned cells' particles (calc_energy, kernel.cu:452-470, as an
+ * O(N) cell-list sum; pairs across the slab boundary count half on each side). */
+int pmc_energy(pmc_ctx* ctx, double* e_out);
+/* Read and optionally reset the accumulated subsweep statistics (synchronises). */
+int pmc_stats_read(pmc_ctx* ctx, pmc_stats* out, int reset);
+/* Device error flags (bit 0: shift overflow, bit 1: assign overflow, bit 2: assign range);
+ * synchronises; `reset` clears them. */
+int pmc_error_flags(pmc_ctx* ctx, uint32_t* flags, int reset);
+
+/* ---- host mirrors ------------------------------------------------------------------ */
+int pmc_copy_out(pmc_ctx* ctx, float* h_disk, int16_t* h_n);
+int pmc_copy_in(pmc_ctx* ctx, const float* h_disk, const int16_t* h_n);
+int pmc_synchronize(pmc_ctx* ctx);
+
+/* ---- slab decomposition support (multi-GPU, halo == 1) ----------------------------- */
+/* Byte offsets/sizes of a storage z-plane (local z in [-1, nz_local]) inside the disk and
+ * n buffers, for point-to-point halo exchange by the caller (RCCL). */
+int pmc_plane_span(const pmc_ctx* ctx, int z_local, size_t* disk_off, size_t* disk_bytes,
+                   size_t* n_off, size_t* n_bytes);
+
+/* ---- diagnostics ------------------------------------------------------------------ */
+/* Evaluate the deterministic math of pmc_detmath.h on the device for `count` Philox word
+ * quadruples (h_words[4*count]): h_out_f[4*count] = 3 trial-move normals + one LJ pair energy,
+ * h_out_d[2*count] = acceptance threshold + fixed-point energy.  Used by the parity tests to pin
+ * host == device bit equality of every transcendental the kernels use. */
+int pmc_selftest_detmath(const uint32_t* h_words, int count, float* h_out_f, double* h_out_d);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PMC_H */

@@ -1,0 +1,489 @@
+// pmc_api.hip -- host side of the C ABI declared in include/pmc.h.
+//
+// Replaces the reference's host driver (start.cu:169-272 / kernel.cu:566-709): device
+// allocation, kernel launches, the MC step loop and the energy/acceptance observables.  All work
+// is asynchronous on the context stream; only the *_read / copy / synchronize calls block.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "pmc_internal.h"
+#include "../../include/pmc_detmath.h"
+
+using namespace pmc;
+
+struct pmc_ctx {
+    pmc_params P;
+    DevGeom G;
+    int64_t cells = 0;              // storage cells (incl. halo planes)
+    float* disk[2] = {nullptr, nullptr};
+    int16_t* n[2] = {nullptr, nullptr};
+    bool own_state = false;
+    int cur = 0;
+    unsigned long long* stats = nullptr;   // kStatCounters * kStatSlots
+    unsigned long long* eacc = nullptr;    // kStatSlots (energy)
+    uint32_t* flags = nullptr;
+    int32_t* tmp_cnt = nullptr;
+    int32_t* tmp_idx = nullptr;
+    float* d_r = nullptr;
+    int64_t r_cap = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipGraphExec_t graph_exec = nullptr;
+    uint32_t graph_first = 0;
+    int graph_count = 0;
+    int graph_cur = -1;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    g_err = std::string(what) + ": " + hipGetErrorString(e);
+    return PMC_ERR_HIP;
+}
+
+#define PMC_HIP(call)                                   \
+    do {                                                \
+        hipError_t e_ = (call);                         \
+        if (e_ != hipSuccess) return hip_fail(e_, #call); \
+    } while (0)
+
+int normalise(pmc_params* p) {
+    if (p->cps_y == 0) p->cps_y = p->cps_x;
+    if (p->cps_z == 0) p->cps_z = p->cps_x;
+    if (p->nz_local == 0) p->nz_local = p->cps_z;
+    if (p->cps_x < 4 || p->cps_y < 4 || p->cps_z < 4) return fail(PMC_ERR_ARG, "cells per side must be >= 4");
+    if ((p->cps_x | p->cps_y | p->cps_z | p->nz_local | p->z0) & 1)
+        return fail(PMC_ERR_ARG, "cells per side, nz_local and z0 must be even (checkerboard)");
+    if (p->nmax < 1 || p->nmax > 64) return fail(PMC_ERR_ARG, "nmax must be in 1..64");
+    if (p->n_moves < 0) return fail(PMC_ERR_ARG, "n_moves must be >= 0");
+    if (p->halo != 0 && p->halo != 1) return fail(PMC_ERR_ARG, "halo must be 0 or 1");
+    if (!p->halo && (p->nz_local != p->cps_z || p->z0 != 0))
+        return fail(PMC_ERR_ARG, "halo == 0 requires the whole box (nz_local == cps_z, z0 == 0)");
+    if (p->z0 < 0 || p->z0 + p->nz_local > p->cps_z) return fail(PMC_ERR_ARG, "slab outside the box");
+    if (!(p->w > 0.0f) || !(p->sigma >= 0.0f)) return fail(PMC_ERR_ARG, "w must be > 0, sigma >= 0");
+    const int64_t cells = (int64_t)p->cps_x * p->cps_y * (p->nz_local + 2 * p->halo);
+    if (cells * 3 * p->nmax >= (int64_t)1 << 40) return fail(PMC_ERR_ARG, "box too large");
+    if ((int64_t)p->cps_x * p->cps_y * p->cps_z > 0xFFFFFFFFll) return fail(PMC_ERR_ARG, "more than 2^32 cells");
+    if (cells >= ((int64_t)1 << 31)) return fail(PMC_ERR_ARG, "more than 2^31 storage cells");
+    return PMC_OK;
+}
+
+DevGeom make_geom(const pmc_params& p) {
+    DevGeom g;
+    g.cps_x = p.cps_x; g.cps_y = p.cps_y; g.cps_z = p.cps_z;
+    g.nz_local = p.nz_local; g.z0 = p.z0; g.halo = p.halo;
+    g.nmax = p.nmax; g.n_moves = p.n_moves;
+    g.nslot = 8;
+    while (g.nslot < p.nmax) g.nslot <<= 1;
+    g.w = p.w; g.beta = p.beta; g.sigma = p.sigma;
+    g.Lx = (float)p.cps_x * p.w;
+    g.Ly = (float)p.cps_y * p.w;
+    g.Lz = (float)p.cps_z * p.w;
+    g.rc2 = pmc_cutoff_r2(p.w);
+    g.k0 = (uint32_t)p.seed;
+    g.k1 = (uint32_t)(p.seed >> 32);
+    return g;
+}
+
+int64_t icbrt_ceil(int64_t n) {
+    int64_t k = (int64_t)std::cbrt((double)n);
+    while (k > 0 && (k - 1) * (k - 1) * (k - 1) >= n) --k;
+    while (k * k * k < n) ++k;
+    return k;
+}
+
+size_t disk_bytes(const pmc_ctx* c) { return sizeof(float) * 3 * (size_t)c->P.nmax * (size_t)c->cells; }
+size_t n_bytes(const pmc_ctx* c) { return sizeof(int16_t) * (size_t)c->cells; }
+
+void free_state(pmc_ctx* c) {
+    if (c->own_state) {
+        for (int b = 0; b < 2; ++b) {
+            if (c->disk[b]) (void)hipFree(c->disk[b]);
+            if (c->n[b]) (void)hipFree(c->n[b]);
+        }
+    }
+    c->disk[0] = c->disk[1] = nullptr;
+    c->n[0] = c->n[1] = nullptr;
+    c->own_state = false;
+}
+
+void drop_graph(pmc_ctx* c) {
+    if (c->graph_exec) (void)hipGraphExecDestroy(c->graph_exec);
+    c->graph_exec = nullptr;
+    c->graph_count = 0;
+}
+
+int enqueue_sweep(pmc_ctx* c, uint32_t sweep) {
+    const pmc_sweep_plan_t plan = pmc_plan_for_sweep(c->P.seed, sweep, c->P.w);
+    for (int k = 0; k < 8; ++k) {
+        int o[3];
+        pmc_colour_offset(plan.order[k], o);
+        hipError_t e = launch_subsweep(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep,
+                                       c->stats, c->stream);
+        if (e != hipSuccess) return hip_fail(e, "subsweep launch");
+    }
+    hipError_t e = launch_shift(c->G, c->disk[c->cur], c->n[c->cur], c->disk[c->cur ^ 1], c->n[c->cur ^ 1],
+                                plan.f, plan.d, c->flags, c->stream);
+    if (e != hipSuccess) return hip_fail(e, "shift launch");
+    c->cur ^= 1;
+    return PMC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* pmc_last_error(void) { return g_err.c_str(); }
+
+int pmc_create(const pmc_params* params, pmc_ctx** out) {
+    if (!params || !out) return fail(PMC_ERR_ARG, "null argument");
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(PMC_ERR_NODEV, "no HIP device");
+    pmc_params p = *params;
+    int rc = normalise(&p);
+    if (rc) return rc;
+    pmc_ctx* c = new pmc_ctx();
+    c->P = p;
+    c->G = make_geom(p);
+    c->cells = (int64_t)p.cps_x * p.cps_y * (p.nz_local + 2 * p.halo);
+    auto cleanup = [&](int code) { pmc_destroy(c); return code; };
+    hipError_t e;
+    if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
+        return cleanup(hip_fail(e, "hipStreamCreate"));
+    c->own_stream = true;
+    c->own_state = true;
+    for (int b = 0; b < 2; ++b) {
+        if ((e = hipMalloc(&c->disk[b], disk_bytes(c))) != hipSuccess) return cleanup(hip_fail(e, "hipMalloc disk"));
+        if ((e = hipMalloc(&c->n[b], n_bytes(c))) != hipSuccess) return cleanup(hip_fail(e, "hipMalloc n"));
+        if ((e = hipMemset(c->disk[b], 0, disk_bytes(c))) != hipSuccess) return cleanup(hip_fail(e, "hipMemset"));
+        if ((e = hipMemset(c->n[b], 0, n_bytes(c))) != hipSuccess) return cleanup(hip_fail(e, "hipMemset"));
+    }
+    const size_t sb = sizeof(unsigned long long) * kStatCounters * kStatSlots;
+    if ((e = hipMalloc(&c->stats, sb)) != hipSuccess) return cleanup(hip_fail(e, "hipMalloc stats"));
+    if ((e = hipMemset(c->stats, 0, sb)) != hipSuccess) return cleanup(hip_fail(e, "hipMemset"));
+    if ((e = hipMalloc(&c->eacc, sizeof(unsigned long long) * kStatSlots)) != hipSuccess)
+        return cleanup(hip_fail(e, "hipMalloc eacc"));
+    if ((e = hipMalloc(&c->flags, 16)) != hipSuccess) return cleanup(hip_fail(e, "hipMalloc flags"));
+    if ((e = hipMemset(c->flags, 0, 16)) != hipSuccess) return cleanup(hip_fail(e, "hipMemset"));
+    if ((e = hipEventCreate(&c->ev0)) != hipSuccess) return cleanup(hip_fail(e, "hipEventCreate"));
+    if ((e = hipEventCreate(&c->ev1)) != hipSuccess) return cleanup(hip_fail(e, "hipEventCreate"));
+    *out = c;
+    return PMC_OK;
+}
+
+void pmc_destroy(pmc_ctx* c) {
+    if (!c) return;
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    drop_graph(c);
+    free_state(c);
+    if (c->stats) (void)hipFree(c->stats);
+    if (c->eacc) (void)hipFree(c->eacc);
+    if (c->flags) (void)hipFree(c->flags);
+    if (c->tmp_cnt) (void)hipFree(c->tmp_cnt);
+    if (c->tmp_idx) (void)hipFree(c->tmp_idx);
+    if (c->d_r) (void)hipFree(c->d_r);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int pmc_set_stream(pmc_ctx* c, void* stream) {
+    if (!c) return fail(PMC_ERR_ARG, "null ctx");
+    PMC_HIP(hipStreamSynchronize(c->stream));
+    drop_graph(c);
+    if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+    c->stream = (hipStream_t)stream;
+    c->own_stream = false;
+    return PMC_OK;
+}
+
+int pmc_attach_state(pmc_ctx* c, float* disk0, int16_t* n0, float* disk1, int16_t* n1) {
+    if (!c || !disk0 || !n0 || !disk1 || !n1) return fail(PMC_ERR_ARG, "null argument");
+    PMC_HIP(hipStreamSynchronize(c->stream));
+    drop_graph(c);
+    free_state(c);
+    c->disk[0] = disk0; c->n[0] = n0;
+    c->disk[1] = disk1; c->n[1] = n1;
+    c->cur = 0;
+    return PMC_OK;
+}
+
+int pmc_state(pmc_ctx* c, float** disk, int16_t** n) {
+    if (!c) return fail(PMC_ERR_ARG, "null ctx");
+    if (disk) *disk = c->disk[c->cur];
+    if (n) *n = c->n[c->cur];
+    return PMC_OK;
+}
+
+int64_t pmc_storage_cells(const pmc_ctx* c) { return c ? c->cells : -1; }
+
+int pmc_init_r(pmc_ctx* c, int64_t n_atoms, float* d_r) {
+    if (!c || !d_r || n_atoms < 0) return fail(PMC_ERR_ARG, "bad argument");
+    hipError_t e = launch_init_r(c->G, n_atoms, icbrt_ceil(n_atoms), d_r, c->stream);
+    return e == hipSuccess ? PMC_OK : hip_fail(e, "init_r launch");
+}
+
+int pmc_assign(pmc_ctx* c, const float* d_r, int64_t n_atoms, float* d_disk, int16_t* d_n) {
+    if (!c || !d_disk || !d_n || (n_atoms > 0 && !d_r)) return fail(PMC_ERR_ARG, "bad argument");
+    if (!c->tmp_cnt) {
+        PMC_HIP(hipMalloc(&c->tmp_cnt, sizeof(int32_t) * (size_t)c->cells));
+        PMC_HIP(hipMalloc(&c->tmp_idx, sizeof(int32_t) * (size_t)c->cells * (size_t)c->P.nmax));
+    }
+    PMC_HIP(hipMemsetAsync(c->flags, 0, 16, c->stream));
+    hipError_t e = launch_assign(c->G, d_r, n_atoms, d_disk, d_n, c->tmp_cnt, c->tmp_idx, c->flags, c->stream);
+    if (e != hipSuccess) return hip_fail(e, "assign launch");
+    uint32_t fl = 0;
+    PMC_HIP(hipMemcpyAsync(&fl, c->flags, 4, hipMemcpyDeviceToHost, c->stream));
+    PMC_HIP(hipStreamSynchronize(c->stream));
+    if (fl & 4u) return fail(PMC_ERR_RANGE, "assign: particle outside the owned box");
+    if (fl & 2u) return fail(PMC_ERR_OVERFLOW, "assign: cell occupancy exceeds nmax");
+    return PMC_OK;
+}
+
+int pmc_subsweep(pmc_ctx* c, float* d_disk, const int16_t* d_n, const int offset[3], uint32_t sweep) {
+    if (!c || !d_disk || !d_n || !offset) return fail(PMC_ERR_ARG, "bad argument");
+    for (int k = 0; k < 3; ++k)
+        if (offset[k] != 0 && offset[k] != 1) return fail(PMC_ERR_ARG, "offset must be in {0,1}^3");
+    hipError_t e = launch_subsweep(c->G, d_disk, d_n, offset[0], offset[1], offset[2], sweep, c->stats, c->stream);
+    return e == hipSuccess ? PMC_OK : hip_fail(e, "subsweep launch");
+}
+
+int pmc_shift_cells(pmc_ctx* c, const float* din, const int16_t* nin, float* dout, int16_t* nout, int f,
+                    float d) {
+    if (!c || !din || !nin || !dout || !nout) return fail(PMC_ERR_ARG, "null buffer");
+    if (f < 0 || f > 2) return fail(PMC_ERR_ARG, "f must be 0, 1 or 2 (reference draws -1..1: start.cu:251)");
+    if (din == dout || nin == nout) return fail(PMC_ERR_ARG, "shift is double-buffered: in != out");
+    hipError_t e = launch_shift(c->G, din, nin, dout, nout, f, d, c->flags, c->stream);
+    return e == hipSuccess ? PMC_OK : hip_fail(e, "shift launch");
+}
+
+int pmc_sweep_plan(uint64_t seed, uint32_t sweep, float w, int order[8], int* f, float* d) {
+    if (!order || !f || !d) return fail(PMC_ERR_ARG, "null argument");
+    const pmc_sweep_plan_t plan = pmc_plan_for_sweep(seed, sweep, w);
+    for (int k = 0; k < 8; ++k) order[k] = plan.order[k];
+    *f = plan.f;
+    *d = plan.d;
+    return PMC_OK;
+}
+
+int pmc_init_lattice(pmc_ctx* c, int64_t n_atoms) {
+    if (!c || n_atoms < 0) return fail(PMC_ERR_ARG, "bad argument");
+    if (n_atoms > c->r_cap) {
+        if (c->d_r) PMC_HIP(hipFree(c->d_r));
+        c->d_r = nullptr;
+        PMC_HIP(hipMalloc(&c->d_r, sizeof(float) * 3 * (size_t)(n_atoms > 0 ? n_atoms : 1)));
+        c->r_cap = n_atoms;
+    }
+    int rc = pmc_init_r(c, n_atoms, c->d_r);
+    if (rc) return rc;
+    PMC_HIP(hipMemsetAsync(c->n[c->cur], 0, n_bytes(c), c->stream));
+    return pmc_assign(c, c->d_r, n_atoms, c->disk[c->cur], c->n[c->cur]);
+}
+
+int pmc_phase(pmc_ctx* c, int colour, uint32_t sweep) {
+    if (!c || colour < 0 || colour > 7) return fail(PMC_ERR_ARG, "bad argument");
+    int o[3];
+    pmc_colour_offset(colour, o);
+    return pmc_subsweep(c, c->disk[c->cur], c->n[c->cur], o, sweep);
+}
+
+int pmc_shift(pmc_ctx* c, uint32_t sweep) {
+    if (!c) return fail(PMC_ERR_ARG, "null ctx");
+    const pmc_sweep_plan_t plan = pmc_plan_for_sweep(c->P.seed, sweep, c->P.w);
+    int rc = pmc_shift_cells(c, c->disk[c->cur], c->n[c->cur], c->disk[c->cur ^ 1], c->n[c->cur ^ 1], plan.f,
+                             plan.d);
+    if (rc) return rc;
+    c->cur ^= 1;
+    return PMC_OK;
+}
+
+int pmc_sweep(pmc_ctx* c, uint32_t sweep) {
+    if (!c) return fail(PMC_ERR_ARG, "null ctx");
+    if (c->P.halo) return fail(PMC_ERR_ARG, "pmc_sweep needs the whole box; slabs use pmc_phase/pmc_shift + halo exchange");
+    return enqueue_sweep(c, sweep);
+}
+
+int pmc_run_graph(pmc_ctx* c, uint32_t first, int count) {
+    if (!c || count < 0) return fail(PMC_ERR_ARG, "bad argument");
+    if (c->P.halo) return fail(PMC_ERR_ARG, "graph replay needs the whole box");
+    if (count == 0) return PMC_OK;
+    // The sweep plan (colour order, f, d) differs per sweep and is baked into kernel arguments,
+    // so the captured graph covers exactly sweeps [first, first+count) from the current buffer.
+    if (!(c->graph_exec && c->graph_first == first && c->graph_count == count && c->graph_cur == c->cur)) {
+        drop_graph(c);
+        hipGraph_t graph = nullptr;
+        const int cur0 = c->cur;
+        PMC_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+        int rc = PMC_OK;
+        for (int k = 0; k < count && rc == PMC_OK; ++k) rc = enqueue_sweep(c, first + (uint32_t)k);
+        hipError_t e = hipStreamEndCapture(c->stream, &graph);
+        c->cur = cur0;
+        if (rc) { if (graph) (void)hipGraphDestroy(graph); return rc; }
+        if (e != hipSuccess) return hip_fail(e, "hipStreamEndCapture");
+        e = hipGraphInstantiate(&c->graph_exec, graph, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(graph);
+        if (e != hipSuccess) return hip_fail(e, "hipGraphInstantiate");
+        c->graph_first = first;
+        c->graph_count = count;
+        c->graph_cur = cur0;
+    }
+    PMC_HIP(hipGraphLaunch(c->graph_exec, c->stream));
+    if (count & 1) c->cur ^= 1;
+    return PMC_OK;
+}
+
+int pmc_energy(pmc_ctx* c, double* e_out) {
+    if (!c || !e_out) return fail(PMC_ERR_ARG, "bad argument");
+    PMC_HIP(hipMemsetAsync(c->eacc, 0, sizeof(unsigned long long) * kStatSlots, c->stream));
+    hipError_t e = launch_energy(c->G, c->disk[c->cur], c->n[c->cur], c->eacc, c->stream);
+    if (e != hipSuccess) return hip_fail(e, "energy launch");
+    std::vector<unsigned long long> h(kStatSlots);
+    PMC_HIP(hipMemcpyAsync(h.data(), c->eacc, sizeof(unsigned long long) * kStatSlots, hipMemcpyDeviceToHost,
+                           c->stream));
+    PMC_HIP(hipStreamSynchronize(c->stream));
+    unsigned long long s = 0;
+    for (auto v : h) s += v;
+    *e_out = (double)(int64_t)s / PMC_FIX_SCALE * 0.5;
+    return PMC_OK;
+}
+
+int pmc_stats_read(pmc_ctx* c, pmc_stats* out, int reset) {
+    if (!c || !out) return fail(PMC_ERR_ARG, "bad argument");
+    std::vector<unsigned long long> h((size_t)kStatCounters * kStatSlots);
+    PMC_HIP(hipMemcpyAsync(h.data(), c->stats, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost,
+                           c->stream));
+    PMC_HIP(hipStreamSynchronize(c->stream));
+    unsigned long long s[kStatCounters] = {0, 0, 0, 0};
+    for (int k = 0; k < kStatCounters; ++k)
+        for (int i = 0; i < kStatSlots; ++i) s[k] += h[(size_t)k * kStatSlots + i];
+    out->de_fixed = (int64_t)s[0];
+    out->accepted = (int64_t)s[1];
+    out->trials = (int64_t)s[2];
+    out->evaluated = (int64_t)s[3];
+    if (reset) {
+        PMC_HIP(hipMemsetAsync(c->stats, 0, sizeof(unsigned long long) * h.size(), c->stream));
+        PMC_HIP(hipStreamSynchronize(c->stream));
+    }
+    return PMC_OK;
+}
+
+int pmc_error_flags(pmc_ctx* c, uint32_t* flags, int reset) {
+    if (!c || !flags) return fail(PMC_ERR_ARG, "bad argument");
+    PMC_HIP(hipMemcpyAsync(flags, c->flags, 4, hipMemcpyDeviceToHost, c->stream));
+    if (reset) PMC_HIP(hipMemsetAsync(c->flags, 0, 16, c->stream));
+    PMC_HIP(hipStreamSynchronize(c->stream));
+    return PMC_OK;
+}
+
+int pmc_start(pmc_ctx* c, uint32_t first, int mc_passes, pmc_result* out) {
+    if (!c || mc_passes < 0) return fail(PMC_ERR_ARG, "bad argument");
+    if (c->P.halo) return fail(PMC_ERR_ARG, "pmc_start drives the whole box; use the slab driver for halo mode");
+    pmc_result r;
+    std::memset(&r, 0, sizeof(r));
+    pmc_stats s0;
+    int rc = pmc_stats_read(c, &s0, 0);
+    if (rc) return rc;
+    rc = pmc_energy(c, &r.e_initial);
+    if (rc) return rc;
+    PMC_HIP(hipEventRecord(c->ev0, c->stream));
+    for (int k = 0; k < mc_passes; ++k) {
+        rc = enqueue_sweep(c, first + (uint32_t)k);
+        if (rc) return rc;
+    }
+    PMC_HIP(hipEventRecord(c->ev1, c->stream));
+    PMC_HIP(hipEventSynchronize(c->ev1));
+    float ms = 0.0f;
+    PMC_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    r.seconds = ms * 1e-3;
+    rc = pmc_energy(c, &r.e_final);
+    if (rc) return rc;
+    pmc_stats s1;
+    rc = pmc_stats_read(c, &s1, 0);
+    if (rc) return rc;
+    r.stats.de_fixed = s1.de_fixed - s0.de_fixed;
+    r.stats.accepted = s1.accepted - s0.accepted;
+    r.stats.trials = s1.trials - s0.trials;
+    r.stats.evaluated = s1.evaluated - s0.evaluated;
+    r.sweeps = mc_passes;
+    uint32_t fl = 0;
+    rc = pmc_error_flags(c, &fl, 0);
+    if (rc) return rc;
+    if (out) *out = r;
+    if (fl & 1u) return fail(PMC_ERR_OVERFLOW, "shiftCells: cell occupancy exceeded nmax");
+    return PMC_OK;
+}
+
+int pmc_copy_out(pmc_ctx* c, float* h_disk, int16_t* h_n) {
+    if (!c) return fail(PMC_ERR_ARG, "null ctx");
+    if (h_disk) PMC_HIP(hipMemcpyAsync(h_disk, c->disk[c->cur], disk_bytes(c), hipMemcpyDeviceToHost, c->stream));
+    if (h_n) PMC_HIP(hipMemcpyAsync(h_n, c->n[c->cur], n_bytes(c), hipMemcpyDeviceToHost, c->stream));
+    PMC_HIP(hipStreamSynchronize(c->stream));
+    return PMC_OK;
+}
+
+int pmc_copy_in(pmc_ctx* c, const float* h_disk, const int16_t* h_n) {
+    if (!c) return fail(PMC_ERR_ARG, "null ctx");
+    if (h_disk) PMC_HIP(hipMemcpyAsync(c->disk[c->cur], h_disk, disk_bytes(c), hipMemcpyHostToDevice, c->stream));
+    if (h_n) PMC_HIP(hipMemcpyAsync(c->n[c->cur], h_n, n_bytes(c), hipMemcpyHostToDevice, c->stream));
+    PMC_HIP(hipStreamSynchronize(c->stream));
+    return PMC_OK;
+}
+
+int pmc_synchronize(pmc_ctx* c) {
+    if (!c) return fail(PMC_ERR_ARG, "null ctx");
+    PMC_HIP(hipStreamSynchronize(c->stream));
+    return PMC_OK;
+}
+
+int pmc_plane_span(const pmc_ctx* c, int z_local, size_t* disk_off, size_t* disk_b, size_t* n_off,
+                   size_t* n_b) {
+    if (!c) return fail(PMC_ERR_ARG, "null ctx");
+    const int lo = -c->P.halo, hi = c->P.nz_local - 1 + c->P.halo;
+    if (z_local < lo || z_local > hi) return fail(PMC_ERR_ARG, "plane outside storage");
+    const size_t plane_cells = (size_t)c->P.cps_x * (size_t)c->P.cps_y;
+    const size_t pidx = (size_t)(z_local + c->P.halo);
+    if (disk_off) *disk_off = pidx * plane_cells * 3 * (size_t)c->P.nmax * sizeof(float);
+    if (disk_b) *disk_b = plane_cells * 3 * (size_t)c->P.nmax * sizeof(float);
+    if (n_off) *n_off = pidx * plane_cells * sizeof(int16_t);
+    if (n_b) *n_b = plane_cells * sizeof(int16_t);
+    return PMC_OK;
+}
+
+int pmc_selftest_detmath(const uint32_t* h_words, int count, float* h_out_f, double* h_out_d) {
+    if (!h_words || !h_out_f || !h_out_d || count < 0) return fail(PMC_ERR_ARG, "bad argument");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(PMC_ERR_NODEV, "no HIP device");
+    if (count == 0) return PMC_OK;
+    uint32_t* dw = nullptr;
+    float* df = nullptr;
+    double* dd = nullptr;
+    PMC_HIP(hipMalloc(&dw, sizeof(uint32_t) * 4 * (size_t)count));
+    PMC_HIP(hipMalloc(&df, sizeof(float) * 4 * (size_t)count));
+    PMC_HIP(hipMalloc(&dd, sizeof(double) * 2 * (size_t)count));
+    PMC_HIP(hipMemcpy(dw, h_words, sizeof(uint32_t) * 4 * (size_t)count, hipMemcpyHostToDevice));
+    hipError_t e = launch_selftest(dw, count, df, dd, pmc_cutoff_r2(2.5f), nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(h_out_f, df, sizeof(float) * 4 * (size_t)count, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(h_out_d, dd, sizeof(double) * 2 * (size_t)count, hipMemcpyDeviceToHost);
+    (void)hipFree(dw);
+    (void)hipFree(df);
+    (void)hipFree(dd);
+    return e == hipSuccess ? PMC_OK : hip_fail(e, "selftest");
+}
+
+}  // extern "C"

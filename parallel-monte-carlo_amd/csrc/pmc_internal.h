@@ -1,0 +1,38 @@
+// pmc_internal.h -- shared between the kernel TU (pmc_kernels.hip) and the host API TU
+// (pmc_api.hip).  Not part of the public C ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/pmc.h"
+
+namespace pmc {
+
+constexpr int kWave = 64;          // CDNA wavefront
+constexpr int kSubWaves = 4;       // cells (waves) per subsweep workgroup
+constexpr int kStatSlots = 1024;   // stats accumulator slots per counter (contention spread)
+constexpr int kStatCounters = 4;   // de_fixed, accepted, trials, evaluated
+
+// Flattened kernel parameters (passed by value).
+struct DevGeom {
+    int cps_x, cps_y, cps_z, nz_local, z0, halo, nmax, n_moves;
+    int nslot;                     // power of two >= nmax (lanes per cell in shift/energy)
+    float w, beta, sigma, Lx, Ly, Lz, rc2;
+    uint32_t k0, k1;
+};
+
+// Launchers (pmc_kernels.hip).  All asynchronous on `st`.
+hipError_t launch_subsweep(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
+                           uint32_t sweep, unsigned long long* stats, hipStream_t st);
+hipError_t launch_shift(const DevGeom& g, const float* din, const int16_t* nin, float* dout,
+                        int16_t* nout, int f, float d, uint32_t* flags, hipStream_t st);
+hipError_t launch_init_r(const DevGeom& g, int64_t n_atoms, int64_t n_cube, float* r, hipStream_t st);
+hipError_t launch_assign(const DevGeom& g, const float* r, int64_t n_atoms, float* disk, int16_t* n,
+                         int32_t* tmp_cnt, int32_t* tmp_idx, uint32_t* flags, hipStream_t st);
+hipError_t launch_energy(const DevGeom& g, const float* disk, const int16_t* n,
+                         unsigned long long* acc, hipStream_t st);
+hipError_t launch_selftest(const uint32_t* words, int count, float* out_f, double* out_d,
+                           float rc2, hipStream_t st);
+
+}  // namespace pmc

@@ -1,0 +1,179 @@
+"""Host-side mirror of the reference call surface over the C ABI (include/pmc.h).
+
+Reference entry points (qingye3/parallel-monte-carlo):
+  init_r(float* r, int N_cube)                     start.cu:47   -> PmcContext.init_r
+  assign(float* r, float* disk, short* n)          start.cu:87   -> PmcContext.assign
+  subsweep_kernel(float* disk, short* n, int* off) subsweep.h:240 -> PmcContext.subsweep_kernel
+  shiftCells(float* disk, short* n, int f, float d) shiftCells.h:28 -> PmcContext.shiftCells
+  main (the `start` program)                       start.cu:169  -> PmcContext.start
+
+Buffers passed to the reference-kernel methods are device pointers (ints) or torch CUDA tensors
+in the reference layout; the driver methods act on the context-owned state.  Every call goes to
+the HIP library -- there is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import numpy as np
+
+from ._lib import Params, Result, Stats, check, lib
+
+FIX_SCALE = 2.0 ** 32
+
+
+def _ptr(x) -> int:
+    if x is None:
+        return 0
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        if not x.is_cuda:
+            raise ValueError("device buffer expected (torch CUDA tensor or device pointer)")
+        return int(x.data_ptr())
+    raise TypeError(f"cannot take a device pointer of {type(x)!r}")
+
+
+def colour_offset(colour: int):
+    """itoa (start.cu:153-157): colour id -> (ox, oy, oz)."""
+    return ((colour // 4) % 2, (colour // 2) % 2, colour % 2)
+
+
+class PmcContext:
+    """One simulation box (or z-slab of one) on the current HIP device."""
+
+    def __init__(self, cps: int = 4, *, cps_y: int = 0, cps_z: int = 0, nz_local: int = 0, z0: int = 0,
+                 halo: int = 0, nmax: int = 16, n_moves: int = 10, w: float = 2.5, beta: float = 0.3,
+                 sigma: float = 0.5, seed: int = 1234, stream: Optional[int] = None):
+        self.params = Params(cps, cps_y, cps_z, nz_local, z0, halo, nmax, n_moves, w, beta, sigma, 0, seed)
+        h = C.c_void_p()
+        check("pmc_create", lib().pmc_create(C.byref(self.params), C.byref(h)))
+        self._h = h
+        self.cps_x = cps
+        self.cps_y = cps_y or cps
+        self.cps_z = cps_z or cps
+        self.nz_local = nz_local or self.cps_z
+        self.z0 = z0
+        self.halo = halo
+        self.nmax = nmax
+        self.n_moves = n_moves
+        self.w = w
+        self.cells = int(lib().pmc_storage_cells(self._h))
+        if stream is not None:
+            self.set_stream(stream)
+
+    # ---- lifecycle ----------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().pmc_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def set_stream(self, stream: int):
+        check("pmc_set_stream", lib().pmc_set_stream(self._h, C.c_void_p(stream)))
+
+    def attach_state(self, disk0, n0, disk1, n1):
+        check("pmc_attach_state", lib().pmc_attach_state(self._h, _ptr(disk0), _ptr(n0), _ptr(disk1), _ptr(n1)))
+
+    def state_ptrs(self):
+        d, n = C.c_void_p(), C.c_void_p()
+        check("pmc_state", lib().pmc_state(self._h, C.byref(d), C.byref(n)))
+        return d.value, n.value
+
+    # ---- reference kernels -------------------------------------------------------------
+    def init_r(self, n_atoms: int, r) -> None:
+        check("pmc_init_r", lib().pmc_init_r(self._h, n_atoms, _ptr(r)))
+
+    def assign(self, r, n_atoms: int, disk, n) -> None:
+        check("pmc_assign", lib().pmc_assign(self._h, _ptr(r), n_atoms, _ptr(disk), _ptr(n)))
+
+    def subsweep_kernel(self, disk, n, offset, sweep: int) -> None:
+        off = (C.c_int * 3)(*[int(v) for v in offset])
+        check("pmc_subsweep", lib().pmc_subsweep(self._h, _ptr(disk), _ptr(n), C.byref(off), sweep))
+
+    def shiftCells(self, disk_in, n_in, disk_out, n_out, f: int, d: float) -> None:  # noqa: N802
+        check("pmc_shift_cells", lib().pmc_shift_cells(self._h, _ptr(disk_in), _ptr(n_in), _ptr(disk_out),
+                                                       _ptr(n_out), f, d))
+
+    # ---- driver ------------------------------------------------------------------------
+    def init_lattice(self, n_atoms: int) -> None:
+        check("pmc_init_lattice", lib().pmc_init_lattice(self._h, n_atoms))
+
+    def sweep(self, s: int) -> None:
+        check("pmc_sweep", lib().pmc_sweep(self._h, s))
+
+    def phase(self, colour: int, s: int) -> None:
+        check("pmc_phase", lib().pmc_phase(self._h, colour, s))
+
+    def shift(self, s: int) -> None:
+        check("pmc_shift", lib().pmc_shift(self._h, s))
+
+    def start(self, first: int, passes: int) -> dict:
+        r = Result()
+        check("pmc_start", lib().pmc_start(self._h, first, passes, C.byref(r)))
+        out = r.stats.as_dict()
+        out.update(e_initial=r.e_initial, e_final=r.e_final, seconds=r.seconds, sweeps=int(r.sweeps))
+        return out
+
+    def run_graph(self, first: int, count: int) -> None:
+        check("pmc_run_graph", lib().pmc_run_graph(self._h, first, count))
+
+    # ---- observables / mirrors ---------------------------------------------------------
+    def energy(self) -> float:
+        e = C.c_double()
+        check("pmc_energy", lib().pmc_energy(self._h, C.byref(e)))
+        return e.value
+
+    def stats(self, reset: bool = False) -> dict:
+        s = Stats()
+        check("pmc_stats_read", lib().pmc_stats_read(self._h, C.byref(s), int(reset)))
+        return s.as_dict()
+
+    def error_flags(self, reset: bool = False) -> int:
+        f = C.c_uint32()
+        check("pmc_error_flags", lib().pmc_error_flags(self._h, C.byref(f), int(reset)))
+        return f.value
+
+    def synchronize(self) -> None:
+        check("pmc_synchronize", lib().pmc_synchronize(self._h))
+
+    def copy_out(self):
+        disk = np.empty(self.cells * 3 * self.nmax, np.float32)
+        n = np.empty(self.cells, np.int16)
+        check("pmc_copy_out", lib().pmc_copy_out(self._h, disk.ctypes.data, n.ctypes.data))
+        return disk, n
+
+    def copy_in(self, disk: np.ndarray, n: np.ndarray) -> None:
+        disk = np.ascontiguousarray(disk, np.float32)
+        n = np.ascontiguousarray(n, np.int16)
+        assert disk.size == self.cells * 3 * self.nmax and n.size == self.cells
+        check("pmc_copy_in", lib().pmc_copy_in(self._h, disk.ctypes.data, n.ctypes.data))
+
+    def plane_span(self, z_local: int):
+        a, b, c, d = C.c_size_t(), C.c_size_t(), C.c_size_t(), C.c_size_t()
+        check("pmc_plane_span", lib().pmc_plane_span(self._h, z_local, C.byref(a), C.byref(b), C.byref(c),
+                                                     C.byref(d)))
+        return a.value, b.value, c.value, d.value
+
+
+def selftest_detmath(words: np.ndarray):
+    """Device evaluation of pmc_detmath.h on Philox word quadruples (diagnostic)."""
+    words = np.ascontiguousarray(words, np.uint32).reshape(-1, 4)
+    cnt = words.shape[0]
+    out_f = np.empty(4 * cnt, np.float32)
+    out_d = np.empty(2 * cnt, np.float64)
+    check("pmc_selftest_detmath", lib().pmc_selftest_detmath(words.ctypes.data, cnt, out_f.ctypes.data,
+                                                             out_d.ctypes.data))
+    return out_f.reshape(cnt, 4), out_d.reshape(cnt, 2)

@@ -1,0 +1,30 @@
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "parallel-monte-carlo_amd")
+ORACLE = os.path.join(REPO, "oracle")
+for p in (PKG, ORACLE, REPO):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")
+    config.addinivalue_line("markers", "slow: long-running statistical test")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    import pmc_oracle
+    pmc_oracle.build()
+    return pmc_oracle
+
+
+@pytest.fixture(scope="session")
+def pmc():
+    import pmc_amd
+    pmc_amd.build()
+    return pmc_amd

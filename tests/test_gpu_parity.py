@@ -1,0 +1,172 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the CPU oracle, bit for bit.
+
+Tolerance: none -- disk/n occupied slots, acceptance counters and the fixed-point energy sums
+must be identical (bitwise), which is stricter than the north-star's 1e-6 relative bound on
+mean energy and acceptance.  Sizes: BASELINE.json configs 1-3 (16^3/1e4, 64^3/1e6, 128^3/1e7).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _ctx(pmc, cps, **kw):
+    return pmc.PmcContext(cps, **kw)
+
+
+def _ostate(oracle, cps, **kw):
+    return oracle.OracleState(oracle.make_params(cps=cps, **kw))
+
+
+def _assert_same(oracle, ctx, st, nmax, sl=None):
+    disk, n = ctx.copy_out()
+    assert np.array_equal(n if sl is None else n[sl], st.n if sl is None else st.n[sl]), "cell counts differ"
+    assert oracle.valid_slots_equal(disk, n, st.disk, st.n, nmax, sl), "particle coordinates differ"
+
+
+def test_detmath_device_equals_host(pmc, oracle):
+    rng = np.random.default_rng(7)
+    words = rng.integers(0, 2**32, size=(20000, 4), dtype=np.uint64).astype(np.uint32)
+    words[:4] = [[0, 0, 0, 0], [0xFFFFFFFF] * 4, [0x200, 0x1FF, 0x80000000, 0x7FFFFFFF], [1, 2, 3, 4]]
+    out_f, out_d = pmc.selftest_detmath(words)
+    rc2 = oracle.cutoff_r2(2.5)
+    import ctypes as C
+    for i in range(0, len(words), 97):
+        w = [int(v) for v in words[i]]
+        g = (C.c_float * 3)()
+        oracle.lib().orc_move_normals(C.byref((C.c_uint32 * 4)(*w)), C.byref(g))
+        assert np.float32(g[0]).view(np.uint32) == out_f[i, 0].view(np.uint32)
+        assert np.float32(g[1]).view(np.uint32) == out_f[i, 1].view(np.uint32)
+        assert np.float32(g[2]).view(np.uint32) == out_f[i, 2].view(np.uint32)
+        u = lambda x: np.float32(((x >> 9) * 2 + 1) * 2.0**-24)  # noqa: E731
+        dx, dy, dz = (np.float32(u(w[k]) * np.float32(5.0) - np.float32(2.5)) for k in (1, 2, 3))
+        e = oracle.pair_energy(float(dx), float(dy), float(dz), rc2)
+        assert np.float32(e).view(np.uint32) == out_f[i, 3].view(np.uint32)
+        T = -oracle.det_log(float(u(w[0])))
+        assert np.float64(T).view(np.uint64) == out_d[i, 0].view(np.uint64)
+        assert oracle.lib().orc_to_fixed(float(out_f[i, 3])) == int(out_d[i, 1])
+
+
+@pytest.mark.parametrize("cps,atoms", [(16, 10_000), (64, 1_000_000)])
+def test_lattice_assign_parity(pmc, oracle, cps, atoms):
+    ctx = _ctx(pmc, cps)
+    ctx.init_lattice(atoms)
+    st = _ostate(oracle, cps)
+    assert st.init_lattice(atoms) == 0
+    _assert_same(oracle, ctx, st, 16)
+    assert int(st.n.sum()) == atoms
+
+
+def test_all_colour_phases_parity_16(pmc, oracle):
+    ctx = _ctx(pmc, 16)
+    ctx.init_lattice(10_000)
+    st = _ostate(oracle, 16)
+    st.init_lattice(10_000)
+    for sweep in (0, 5):
+        for colour in range(8):
+            ctx.phase(colour, sweep)
+            st.subsweep(oracle.colour_offset(colour), sweep)
+            _assert_same(oracle, ctx, st, 16)
+    s = ctx.stats()
+    o = st.stats.as_dict()
+    assert s == o, (s, o)
+    assert s["trials"] > 0 and 0 < s["accepted"] < s["evaluated"] < s["trials"]
+
+
+@pytest.mark.parametrize("f,d", [(0, 0.7), (1, -1.1), (2, 1.2499), (2, -1.25), (0, -1e-7)])
+def test_shift_parity(pmc, oracle, f, d):
+    import torch
+    ctx = _ctx(pmc, 16)
+    ctx.init_lattice(10_000)
+    ctx.start(0, 2)  # decorrelate from the lattice
+    disk, n = ctx.copy_out()
+    st = _ostate(oracle, 16)
+    st.disk[:] = disk
+    st.n[:] = n
+    dev = torch.device("cuda")
+    din = torch.from_numpy(disk).to(dev)
+    nin = torch.from_numpy(n).to(dev)
+    dout = torch.zeros_like(din)
+    nout = torch.zeros_like(nin)
+    ctx.shiftCells(din, nin, dout, nout, f, d)
+    ctx.synchronize()
+    assert st.shift_cells(f, d) == 0
+    got_d, got_n = dout.cpu().numpy(), nout.cpu().numpy()
+    assert np.array_equal(got_n, st.n)
+    assert oracle.valid_slots_equal(got_d, got_n, st.disk, st.n, 16)
+    assert int(got_n.sum()) == 10_000
+
+
+def test_full_sweeps_parity_16(pmc, oracle):
+    ctx = _ctx(pmc, 16)
+    ctx.init_lattice(10_000)
+    st = _ostate(oracle, 16)
+    st.init_lattice(10_000)
+    r = ctx.start(0, 6)
+    assert st.run(0, 6) == 0
+    _assert_same(oracle, ctx, st, 16)
+    o = st.stats.as_dict()
+    for k in ("de_fixed", "accepted", "trials", "evaluated"):
+        assert r[k] == o[k], k
+    assert r["e_final"] == st.energy()
+    # energy bookkeeping: E_final ~= E_initial + sum(accepted dE) (float rounding only)
+    assert abs(r["e_initial"] + r["de_fixed"] / 2**32 - r["e_final"]) < 1e-3 * abs(r["e_final"])
+
+
+def test_graph_replay_equals_eager(pmc):
+    a = _ctx(pmc, 16)
+    b = _ctx(pmc, 16)
+    a.init_lattice(10_000)
+    b.init_lattice(10_000)
+    for s in range(4):
+        a.sweep(s)
+    b.run_graph(0, 4)
+    da, na = a.copy_out()
+    db, nb = b.copy_out()
+    assert np.array_equal(na, nb) and np.array_equal(da.view(np.uint32), db.view(np.uint32))
+    assert a.stats() == b.stats()
+
+
+def test_single_colour_parity_64(pmc, oracle):
+    """BASELINE config 2: 64^3 cells, 1e6 particles, one colour phase."""
+    ctx = _ctx(pmc, 64)
+    ctx.init_lattice(1_000_000)
+    st = _ostate(oracle, 64)
+    st.init_lattice(1_000_000)
+    oracle.set_threads(8)
+    ctx.phase(5, 3)
+    st.subsweep(oracle.colour_offset(5), 3)
+    _assert_same(oracle, ctx, st, 16)
+    assert ctx.stats() == st.stats.as_dict()
+
+
+def test_single_colour_parity_128(pmc, oracle):
+    """BASELINE config 3 size: 128^3 cells, 1e7 particles; one colour phase compared bitwise,
+    then size-independent properties over full sweeps."""
+    ctx = _ctx(pmc, 128)
+    ctx.init_lattice(10_000_000)
+    st = _ostate(oracle, 128)
+    st.init_lattice(10_000_000)
+    _assert_same(oracle, ctx, st, 16)
+    oracle.set_threads(16)
+    ctx.phase(2, 11)
+    st.subsweep(oracle.colour_offset(2), 11)
+    _assert_same(oracle, ctx, st, 16)
+    assert ctx.stats(reset=True) == st.stats.as_dict()
+    # full sweeps: particle conservation, every particle inside its cell's closed box, E bookkeeping
+    e0 = ctx.energy()
+    r = ctx.start(20, 3)
+    disk, n = ctx.copy_out()
+    assert int(n.sum()) == 10_000_000
+    assert ctx.error_flags() == 0
+    d3 = disk.reshape(-1, 3, 16)
+    idx = np.arange(128**3)
+    cx, cy, cz = idx % 128, (idx // 128) % 128, idx // (128 * 128)
+    mask = np.arange(16)[None, :] < n[:, None]
+    for k, cc in enumerate((cx, cy, cz)):
+        lb = (cc * 2.5 - 160.0).astype(np.float32)[:, None]
+        v = d3[:, k, :]
+        assert np.all((v[mask] >= np.broadcast_to(lb, v.shape)[mask]) &
+                      (v[mask] <= np.broadcast_to(lb + 2.5, v.shape)[mask]))
+    assert r["e_initial"] == pytest.approx(e0)
+    assert abs(r["e_initial"] + r["de_fixed"] / 2**32 - r["e_final"]) < 1e-4 * abs(r["e_final"])

@@ -1,0 +1,226 @@
+"""CPU tests of the oracle: pinned against the reference's own data file (dumpR3.txt frames),
+lattice energies derived from the reference's definitions, published Philox KATs and the
+statistical known answer of the N=64 model."""
+import math
+import os
+
+import numpy as np
+import pytest
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "dumpR3_frames.npz")
+
+
+# ---------------------------------------------------------------------------------------------
+# primitives
+# ---------------------------------------------------------------------------------------------
+def test_philox_kat(oracle):
+    # Random123 kat_vectors, philox4x32_10
+    assert oracle.philox([0, 0, 0, 0], [0, 0]) == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
+    assert oracle.philox([0xFFFFFFFF] * 4, [0xFFFFFFFF] * 2) == [0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD]
+    assert oracle.philox([0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344], [0xA4093822, 0x299F31D0]) == \
+        [0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1]
+
+
+def test_det_log_accuracy(oracle):
+    rng = np.random.default_rng(1)
+    xs = np.concatenate([rng.random(2000), [2.0**-24, 0.5, 0.70710678, 0.9999999, 1.0 - 2.0**-24]])
+    for x in xs:
+        x = float(x)
+        if x <= 0:
+            continue
+        ref = math.log(x)
+        assert abs(oracle.det_log(x) - ref) <= 4e-16 * max(1.0, abs(ref))
+
+
+def test_det_sincos_accuracy(oracle):
+    for k in range(0, 2**23, 2**23 // 997):
+        u = float(np.float32((2 * k + 1) * 2.0**-24))
+        s, c = oracle.det_sincos_2pi(u)
+        assert abs(s - math.sin(2 * math.pi * u)) < 1.2e-7
+        assert abs(c - math.cos(2 * math.pi * u)) < 1.2e-7
+
+
+def test_normals_moments(oracle):
+    import ctypes as C
+    g = (C.c_float * 3)()
+    vals = []
+    for i in range(20000):
+        w = oracle.philox([i, 7, 0, 0], [1234, 0])
+        oracle.lib().orc_move_normals(C.byref((C.c_uint32 * 4)(*w)), C.byref(g))
+        vals.extend(g)
+    v = np.array(vals)
+    assert abs(v.mean()) < 0.02 and abs(v.std() - 1) < 0.02
+    assert abs(np.mean(v**4) - 3) < 0.15
+
+
+def test_pair_energy_and_cutoff(oracle):
+    rc2 = oracle.cutoff_r2(2.5)
+    # the r^2 cutoff is the reference's sqrtf(r2) > w predicate (subsweep.h:96-99)
+    assert np.sqrt(np.float32(rc2)) <= np.float32(2.5)
+    assert np.sqrt(np.nextafter(np.float32(rc2), np.float32(10))) > np.float32(2.5)
+    for r in (0.9, 1.0, 1.122462, 1.5, 2.0, 2.49):
+        e = oracle.pair_energy(r, 0.0, 0.0, rc2)
+        ref = 4 * (r**-12 - r**-6)
+        assert e == pytest.approx(ref, rel=2e-6, abs=1e-7)
+    assert oracle.pair_energy(2.6, 0.0, 0.0, rc2) == 0.0
+    assert np.isfinite(oracle.pair_energy(0.0, 0.0, 0.0, rc2))
+
+
+def test_sweep_plan(oracle):
+    fs = []
+    for s in range(300):
+        order, f, d = oracle.sweep_plan(1234, s)
+        assert sorted(order) == list(range(8))
+        assert f in (0, 1, 2)
+        assert -1.25 < d < 1.25 and d != 0.0
+        fs.append(f)
+    assert set(fs) == {0, 1, 2}
+    assert oracle.sweep_plan(1234, 3) == oracle.sweep_plan(1234, 3)
+    assert oracle.sweep_plan(1234, 3) != oracle.sweep_plan(1235, 3)
+
+
+def test_fixed_point(oracle):
+    f = oracle.lib().orc_to_fixed
+    assert f(1.0) == 2**32 and f(-1.0) == -(2**32)
+    assert f(0.5 / 2**32) == 1 and f(-0.5 / 2**32) == -1 and f(0.49 / 2**32) == 0
+    assert f(1e30) == 2**62
+
+
+# ---------------------------------------------------------------------------------------------
+# pinned against the reference's data (dumpR3.txt) and definitions
+# ---------------------------------------------------------------------------------------------
+def test_init_r_matches_dumpR3_frame0(oracle):
+    """Frame 0 of the reference trajectory is its init_r lattice for N=64 (kernel.cu:78-89)."""
+    g = np.load(GOLDEN)
+    st = oracle.OracleState(oracle.make_params(cps=4, nmax=10))
+    r = st.init_r(64).reshape(3, 64).T
+    assert np.array_equal(r.astype(np.float64), g["positions"][0])
+
+
+@pytest.mark.parametrize("k", range(5))
+def test_energy_matches_reference_calc_energy(oracle, k):
+    """The cell-list energy equals calc_energy (kernel.cu:452-470) on the reference frames."""
+    g = np.load(GOLDEN)
+    pos = g["positions"][k].astype(np.float32)
+    st = oracle.OracleState(oracle.make_params(cps=4, nmax=10))
+    r = np.ascontiguousarray(pos.T).reshape(-1)
+    assert st.assign(r) == 0
+    assert int(st.n.max()) == int(g["max_occupancy"][k])
+    assert st.energy() == pytest.approx(float(g["energy_calc"][k]), rel=2e-6, abs=2e-6)
+
+
+@pytest.mark.parametrize("atoms,ref", [(64, -3.132843), (800, -2873.914743), (1000, -3982.336447)])
+def test_lattice_energy_known_answers(oracle, atoms, ref):
+    st = oracle.OracleState(oracle.make_params(cps=4, nmax=32))
+    assert st.init_lattice(atoms) == 0
+    assert int(st.n.sum()) == atoms
+    assert st.energy() == pytest.approx(ref, rel=2e-8, abs=2e-6)
+
+
+def test_lattice_cube_root_exact(oracle):
+    """start.cu:208 truncates int(cbrt(float(1e6))) to 99; the build uses the exact cube root."""
+    st = oracle.OracleState(oracle.make_params(cps=8))
+    r = st.init_r(1000).reshape(3, -1)
+    assert len(np.unique(r[0])) == 10
+
+
+# ---------------------------------------------------------------------------------------------
+# algorithm invariants
+# ---------------------------------------------------------------------------------------------
+def _in_cells(st):
+    p = st.p
+    d3 = st.disk3()
+    cps = (p.cps_x, p.cps_y, p.cps_z)
+    idx = np.arange(st.cells)
+    coords = (idx % cps[0], (idx // cps[0]) % cps[1], idx // (cps[0] * cps[1]))
+    mask = np.arange(st.nmax)[None, :] < st.n[:, None]
+    for k in range(3):
+        L = cps[k] * 2.5
+        lb = (coords[k] * 2.5 - L / 2).astype(np.float32)[:, None]
+        v = d3[:, k, :]
+        lbb = np.broadcast_to(lb, v.shape)
+        if not np.all((v[mask] >= lbb[mask]) & (v[mask] <= lbb[mask] + np.float32(2.5))):
+            return False
+    return True
+
+
+def test_subsweep_invariants(oracle):
+    st = oracle.OracleState(oracle.make_params(cps=8))
+    st.init_lattice(1000)
+    n0 = st.n.copy()
+    for colour in range(8):
+        st.subsweep(oracle.colour_offset(colour), 0)
+    assert np.array_equal(st.n, n0)
+    assert _in_cells(st)
+    s = st.stats.as_dict()
+    # fraction of trial moves that stay in the cell: ~ 0.84042^3 for uniform start (SURVEY s.4)
+    assert 0.45 < s["evaluated"] / s["trials"] < 0.75
+    # only colour-phase cells move: a second identical run reproduces bit for bit
+    st2 = oracle.OracleState(oracle.make_params(cps=8))
+    st2.init_lattice(1000)
+    for colour in range(8):
+        st2.subsweep(oracle.colour_offset(colour), 0)
+    assert np.array_equal(st.disk, st2.disk)
+
+
+def test_subsweep_thread_count_invariant(oracle):
+    a = oracle.OracleState(oracle.make_params(cps=16))
+    b = oracle.OracleState(oracle.make_params(cps=16))
+    a.init_lattice(10000)
+    b.init_lattice(10000)
+    oracle.set_threads(0)
+    a.run(0, 2)
+    oracle.set_threads(4)
+    b.run(0, 2)
+    oracle.set_threads(0)
+    assert np.array_equal(a.n, b.n) and oracle.valid_slots_equal(a.disk, a.n, b.disk, b.n, 16)
+    assert a.stats.as_dict() == b.stats.as_dict()
+
+
+@pytest.mark.parametrize("f,d", [(0, 0.9), (1, -0.3), (2, 1.2), (2, -1.2499)])
+def test_shift_is_translation(oracle, f, d):
+    """shiftCells (fixed copy, float s) = translation x_f -> x_f - d (mod L) + re-bin; the
+    root copy's int s[3] breaks this."""
+    st = oracle.OracleState(oracle.make_params(cps=8))
+    st.init_lattice(2000)
+    st.run(0, 3)
+    before = st.positions().astype(np.float64)
+    e0 = st.energy()
+    assert st.shift_cells(f, d) == 0
+    after = st.positions().astype(np.float64)
+    assert len(after) == len(before)
+    assert _in_cells(st)
+    L = 20.0
+    exp = before.copy()
+    exp[:, f] = (exp[:, f] - d + L / 2) % L - L / 2
+    key = lambda a: a[np.lexsort((a[:, 2], a[:, 1], a[:, 0]))]  # noqa: E731
+    diff = np.abs(key(np.round(after, 3)) - key(np.round(exp, 3)))
+    diff = np.minimum(diff, np.abs(diff - L))
+    assert diff.max() < 2e-3
+    assert st.energy() == pytest.approx(e0, rel=1e-5)
+
+
+def test_energy_bookkeeping(oracle):
+    st = oracle.OracleState(oracle.make_params(cps=8))
+    st.init_lattice(2000)
+    e0 = st.energy()
+    st.run(0, 20)
+    e1 = st.energy()
+    assert abs(e0 + st.stats.de_fixed / 2**32 - e1) < 1e-3
+    assert int(st.n.sum()) == 2000
+
+
+def test_mean_energy_known_answer(oracle):
+    """<E> of the N=64, L=10, beta=0.3, sigma=0.5, rc=2.5 model: -21.240 +- 0.022 (textbook
+    Metropolis).  The checkerboard chain must sample the same distribution."""
+    st = oracle.OracleState(oracle.make_params(cps=4))
+    st.init_lattice(64)
+    st.run(0, 500)
+    es = []
+    for s in range(500, 30500, 5):
+        st.run(s, 5)
+        es.append(st.energy())
+    es = np.array(es)
+    blocks = es.reshape(20, -1).mean(1)
+    se = blocks.std(ddof=1) / np.sqrt(len(blocks))
+    assert abs(es.mean() - (-21.240)) < 3 * math.hypot(se, 0.022) + 0.02
