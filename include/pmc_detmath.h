@@ -10,7 +10,7 @@
  *     reference's cuRAND XORWOW stream (curand_init(1234,id,0), subsweep.h:256-259 /
  *     start.cu:532), which is re-seeded on every launch.
  *   - uniform / normal / exponential variates on fixed counter slots.
- *   - det_log (fdlibm-style log, double) and det_sincos_2pi (octant reduction + Taylor).
+ *   - pmc_logf (fdlibm-style log) and pmc_det_sincos_2pi (octant reduction + Taylor), float.
  *   - the Lennard-Jones pair energy (subsweep.h:90-103 semantics, see pmc_pair_energy).
  *   - cell-index and sweep-plan helpers (colour order, shift axis / distance).
  *
@@ -77,69 +77,65 @@ PMC_HD uint32_t pmc_bounded(uint32_t w, uint32_t range) {
 }
 
 /* ------------------------------------------------------------------------------------- */
-/* det_log: natural log of a positive normal double (fdlibm e_log.c algorithm)           */
+/* pmc_logf: natural log of a positive normal float (fdlibm e_logf.c reduction: m in        */
+/* (sqrt(1/2), sqrt(2)], s = f/(2+f), log(1+f) = 2s(1 + s^2/3 + ... + s^8/9)); ~2 ulp.     */
+/* The division is pmc_recip (defined below), so every op is an IEEE op or an fma.         */
 /* ------------------------------------------------------------------------------------- */
-PMC_HD double pmc_det_log(double x) {
-    const double ln2_hi = 6.93147180369123816490e-01;
-    const double ln2_lo = 1.90821492927058770002e-10;
-    const double Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01,
-                 Lg3 = 2.857142874366239149e-01, Lg4 = 2.222219843214978396e-01,
-                 Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
-                 Lg7 = 1.479819860511658591e-01;
-    uint64_t b = pmc_dbits(x);
-    int e = (int)((b >> 52) & 0x7ff) - 1023;
-    double m = pmc_bitsd((b & 0x000fffffffffffffull) | 0x3ff0000000000000ull); /* [1,2) */
-    if (m > 1.4142135623730951) { m = m * 0.5; e += 1; }                      /* exact */
-    double f = m - 1.0;                                                         /* exact */
-    double hfsq = 0.5 * f * f;
-    double s = f / (2.0 + f);
-    double z = s * s;
-    double w = z * z;
-    double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
-    double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
-    double R = t2 + t1;
-    double dk = (double)e;
-    return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+PMC_HD float pmc_recip(float x);
+
+PMC_HD float pmc_logf(float x) {
+    const float ln2_hi = 6.9313812256e-01f;   /* 0x3f317180: trailing zero bits, e*ln2_hi exact */
+    const float ln2_lo = 9.0580006145e-06f;   /* 0x3717f7d1 */
+    uint32_t b = pmc_fbits(x);
+    int e = (int)(b >> 23) - 127;
+    float m = pmc_bitsf((b & 0x007FFFFFu) | 0x3F800000u);  /* [1,2) */
+    if (m > 1.41421356f) { m = m * 0.5f; e += 1; }            /* exact */
+    float f = m - 1.0f;                                       /* exact */
+    float s = f * pmc_recip(2.0f + f);
+    float z = s * s;
+    float P = 1.0f + z * (0.333333343f + z * (0.2f + z * (0.142857149f + z * 0.111111112f)));
+    float r = (2.0f * s) * P;
+    float de = (float)e;
+    return de * ln2_hi + (r + de * ln2_lo);
 }
 
-/* sin / cos of 2*pi*u for u in [0,1) given as a float (so 4u is exact). */
+/* sin / cos of 2*pi*u for u in [0,1) given as a float (so 4u is exact): octant reduction, then
+ * Taylor polynomials on [0, pi/4] (truncation < 2e-9); float ops only. */
 PMC_HD void pmc_det_sincos_2pi(float u, float* s_out, float* c_out) {
     float t = 4.0f * u;              /* exact */
     int q = (int)t;                  /* quadrant 0..3 */
     float r = t - (float)q;          /* exact, [0,1) */
     int comp = r > 0.5f;
     float a = comp ? (1.0f - r) : r; /* exact (Sterbenz), [0, 0.5] */
-    double x = (double)a * 1.5707963267948966;   /* [0, pi/4] */
-    double x2 = x * x;
-    /* Taylor to x^15 / x^16: truncation error < 3e-14 on [0, pi/4] */
-    double sp = 1.0 + x2 * (-1.0 / 6.0 + x2 * (1.0 / 120.0 + x2 * (-1.0 / 5040.0
-              + x2 * (1.0 / 362880.0 + x2 * (-1.0 / 39916800.0 + x2 * (1.0 / 6227020800.0
-              + x2 * (-1.0 / 1307674368000.0)))))));
-    double sx = x * sp;
-    double cx = 1.0 + x2 * (-0.5 + x2 * (1.0 / 24.0 + x2 * (-1.0 / 720.0 + x2 * (1.0 / 40320.0
-              + x2 * (-1.0 / 3628800.0 + x2 * (1.0 / 479001600.0 + x2 * (-1.0 / 87178291200.0
-              + x2 * (1.0 / 20922789888000.0))))))));
-    double sr = comp ? cx : sx;      /* sin(r*pi/2) */
-    double cr = comp ? sx : cx;      /* cos(r*pi/2) */
-    double so, co;
+    float x = a * 1.57079637f;       /* [0, pi/4] */
+    float x2 = x * x;
+    float sp = 1.0f + x2 * (-0.166666672f + x2 * (8.33333377e-03f + x2 * (-1.98412701e-04f
+               + x2 * 2.75573188e-06f)));
+    float sx = x * sp;
+    float cx = 1.0f + x2 * (-0.5f + x2 * (4.16666679e-02f + x2 * (-1.38888892e-03f
+               + x2 * (2.48015876e-05f + x2 * -2.75573192e-07f))));
+    float sr = comp ? cx : sx;       /* sin(r*pi/2) */
+    float cr = comp ? sx : cx;       /* cos(r*pi/2) */
+    float so, co;
     if (q == 0)      { so = sr;  co = cr;  }
     else if (q == 1) { so = cr;  co = -sr; }
     else if (q == 2) { so = -sr; co = -cr; }
     else             { so = -cr; co = sr;  }
-    *s_out = (float)so;
-    *c_out = (float)co;
+    *s_out = so;
+    *c_out = co;
 }
+
+/* Box-Muller radius sqrt(-2 log u) (sqrtf is correctly rounded on both targets). */
+PMC_HD float pmc_bm_radius(float u) { return __builtin_sqrtf(-2.0f * pmc_logf(u)); }
 
 /* Three standard normals for one trial move (two Box-Muller pairs, fourth value dropped).
  * Replaces curand_normal x3 in make_move (subsweep.h:60-71). */
 PMC_HD void pmc_move_normals(pmc_u32x4 w, float* g0, float* g1, float* g2) {
-    float u0 = pmc_u01(w.v[0]), u1 = pmc_u01(w.v[1]);
-    float u2 = pmc_u01(w.v[2]), u3 = pmc_u01(w.v[3]);
-    float r0 = __builtin_sqrtf((float)(-2.0 * pmc_det_log((double)u0)));
-    float r2 = __builtin_sqrtf((float)(-2.0 * pmc_det_log((double)u2)));
+    float r0 = pmc_bm_radius(pmc_u01(w.v[0]));
+    float r2 = pmc_bm_radius(pmc_u01(w.v[2]));
     float s1, c1, s3, c3;
-    pmc_det_sincos_2pi(u1, &s1, &c1);
-    pmc_det_sincos_2pi(u3, &s3, &c3);
+    pmc_det_sincos_2pi(pmc_u01(w.v[1]), &s1, &c1);
+    pmc_det_sincos_2pi(pmc_u01(w.v[3]), &s3, &c3);
     *g0 = r0 * c1;
     *g1 = r0 * s1;
     *g2 = r2 * c3;
@@ -147,10 +143,8 @@ PMC_HD void pmc_move_normals(pmc_u32x4 w, float* g0, float* g1, float* g2) {
 
 /* Acceptance threshold T = -log(u), u in (0,1).  Metropolis test of accept_move
  * (subsweep.h:209-216: accept if dE<0 else if u < exp(-beta dE)) is evaluated as
- * beta*dE < T in double; beta*dE is exact in double (24x24-bit product). */
-PMC_HD double pmc_accept_threshold(pmc_u32x4 w) {
-    return -pmc_det_log((double)pmc_u01(w.v[0]));
-}
+ * (double)beta*(double)dE < (double)T; the product is exact in double. */
+PMC_HD float pmc_accept_threshold(pmc_u32x4 w) { return -pmc_logf(pmc_u01(w.v[0])); }
 
 /* ------------------------------------------------------------------------------------- */
 /* Lennard-Jones pair energy, epsilon = sigma_LJ = 1, truncated (not shifted) at w.       */
@@ -167,13 +161,56 @@ PMC_HD float pmc_r2(float dx, float dy, float dz) {
     return r2 + dz * dz;
 }
 
+/* Reciprocal by three Newton-Raphson steps from a bit-trick seed (max seed error 5.1%,
+ * then 2.6e-3, 6.6e-6, 4.4e-11 before float rounding: ~1 ulp).  Only integer ops and fused
+ * multiply-adds (IEEE, single rounding on both gfx950 v_fma_f32 and x86 vfmadd), so the result
+ * is bit-identical on host and device -- and cheaper on CDNA than a correctly rounded division
+ * (v_div_scale x2 + v_rcp + 4 fma + v_div_fmas + v_div_fixup). */
+PMC_HD float pmc_recip(float x) {
+    float y = pmc_bitsf(0x7EF311C3u - pmc_fbits(x));
+    float e = __builtin_fmaf(-x, y, 1.0f);
+    y = __builtin_fmaf(y, e, y);
+    e = __builtin_fmaf(-x, y, 1.0f);
+    y = __builtin_fmaf(y, e, y);
+    e = __builtin_fmaf(-x, y, 1.0f);
+    y = __builtin_fmaf(y, e, y);
+    return y;
+}
+
 PMC_HD float pmc_lj_from_r2(float r2, float rc2) {
     float rr = r2 < PMC_R2_MIN ? PMC_R2_MIN : r2;
-    float inv = 1.0f / rr;
+    float inv = pmc_recip(rr);
     float p6 = inv * inv * inv;
     float e = 4.0f * (p6 * p6 - p6);
     return r2 <= rc2 ? e : 0.0f;
 }
+
+/* Conservative partner filter (staging): squared distance from a staged partner to the own
+ * cell's closed box [lo, hi] (each side padded by PMC_BOX_PAD).  A partner with
+ * d2 > rc2 * (1 + 2^-13) is farther than the cutoff from every position a particle of the cell
+ * can take, so its pair energy is exactly 0 for every trial move and it is not staged. */
+#define PMC_BOX_PAD 1.0e-3f
+PMC_HD float pmc_box_d2(float x, float y, float z, const float lo[3], const float hi[3]) {
+    /* fmaxf (maxNum): identical on both targets for non-NaN inputs; the sign of a zero is
+     * irrelevant after squaring */
+    float tx = __builtin_fmaxf(__builtin_fmaxf(lo[0] - x, x - hi[0]), 0.0f);
+    float ty = __builtin_fmaxf(__builtin_fmaxf(lo[1] - y, y - hi[1]), 0.0f);
+    float tz = __builtin_fmaxf(__builtin_fmaxf(lo[2] - z, z - hi[2]), 0.0f);
+    float d2 = tx * tx + ty * ty;
+    return d2 + tz * tz;
+}
+
+/* own-cell closed box padded by PMC_BOX_PAD: lb = c*w - L/2.0f (start.cu:129), ub = lb + w */
+PMC_HD void pmc_cell_box(int cx, int cy, int cz, float w, float Lx, float Ly, float Lz, float lo[3],
+                         float hi[3]) {
+    float lbx = (float)cx * w - Lx / 2.0f, lby = (float)cy * w - Ly / 2.0f, lbz = (float)cz * w - Lz / 2.0f;
+    lo[0] = lbx - PMC_BOX_PAD; hi[0] = (lbx + w) + PMC_BOX_PAD;
+    lo[1] = lby - PMC_BOX_PAD; hi[1] = (lby + w) + PMC_BOX_PAD;
+    lo[2] = lbz - PMC_BOX_PAD; hi[2] = (lbz + w) + PMC_BOX_PAD;
+}
+
+/* filter threshold: rc2 * (1 + 2^-13) */
+PMC_HD float pmc_filter_r2(float rc2) { return rc2 * 1.0001220703125f; }
 
 /* Fixed-point energy unit for observables: 2^-32 (order-independent int64 sums). */
 #define PMC_FIX_SCALE 4294967296.0

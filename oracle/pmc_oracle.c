@@ -163,7 +163,7 @@ int orc_assign(const pmc_params* p, const float* r, int64_t n_atoms, float* disk
 /* subsweep                                                                              */
 /* ------------------------------------------------------------------------------------- */
 static void subsweep_cell(const pmc_params* p, float* disk, const int16_t* n, int x, int y, int zl,
-                          uint32_t sweep, float rc2, float* xs, float* ys, float* zs,
+                          uint32_t sweep, float rc2, float* px_, float* py_, float* pz_,
                           int64_t* de, int64_t* acc, int64_t* tri, int64_t* ev) {
     const int nm = p->nmax;
     const int64_t c = sidx(p, x, y, zl);
@@ -171,6 +171,7 @@ static void subsweep_cell(const pmc_params* p, float* disk, const int16_t* n, in
     if (n_own == 0) return;                       /* subsweep.h:252-253 */
     const uint32_t id = gid(p, x, y, zl);
     const uint32_t k0 = (uint32_t)p->seed, k1 = (uint32_t)(p->seed >> 32);
+    const float Lx = (float)p->cps_x * p->w, Ly = (float)p->cps_y * p->w, Lz = (float)p->cps_z * p->w;
 
     /* shuffle (random_shuffle, subsweep.h:50-58; proper Fisher-Yates, fixes R1) */
     int perm[64];
@@ -181,37 +182,44 @@ static void subsweep_cell(const pmc_params* p, float* disk, const int16_t* n, in
         int t = perm[i]; perm[i] = perm[j]; perm[j] = t;
     }
 
-    /* stage own cell (shuffled) then the 26 neighbours (cpy_to_Dsh subsweep.h:18-27 +
-     * calculate_energy_in_neighbors' global reads subsweep.h:153-172; Version II ldisk
-     * staging kernel.cu:241-278) */
+    /* stage the 26 neighbour cells (get_neighbors order, subsweep.h:119-137; global reads of
+     * calculate_energy_in_neighbors :153-172 done once, Version II ldisk staging kernel.cu:269-278),
+     * keeping only partners within the cutoff of the own cell's box (their pair energy is
+     * otherwise exactly 0); then the own cell in shuffled order (cpy_to_Dsh, subsweep.h:18-27). */
     int off[27][3];
     stencil_offsets(off);
+    float lo[3], hi[3];
+    pmc_cell_box(x, y, p->z0 + zl, p->w, Lx, Ly, Lz, lo, hi);
+    const float rcf = pmc_filter_r2(rc2);
     int S = 0;
-    for (int s = 0; s < n_own; ++s) {
-        /* the own cell's image shift is 0; it is added like the neighbours' (x + 0.0f) */
-        xs[S] = disk[c * 3 * nm + perm[s]] + 0.0f;
-        ys[S] = disk[c * 3 * nm + nm + perm[s]] + 0.0f;
-        zs[S] = disk[c * 3 * nm + 2 * nm + perm[s]] + 0.0f;
-        ++S;
-    }
     for (int k = 1; k < 27; ++k) {
         nbref b = nb_of(p, x, y, zl, off[k][0], off[k][1], off[k][2]);
         int cnt = n[b.idx];
         for (int q = 0; q < cnt; ++q) {
-            xs[S] = disk[b.idx * 3 * nm + q] + b.sx;
-            ys[S] = disk[b.idx * 3 * nm + nm + q] + b.sy;
-            zs[S] = disk[b.idx * 3 * nm + 2 * nm + q] + b.sz;
-            ++S;
+            float vx = disk[b.idx * 3 * nm + q] + b.sx;
+            float vy = disk[b.idx * 3 * nm + nm + q] + b.sy;
+            float vz = disk[b.idx * 3 * nm + 2 * nm + q] + b.sz;
+            if (pmc_box_d2(vx, vy, vz, lo, hi) <= rcf) {
+                px_[S] = vx; py_[S] = vy; pz_[S] = vz;
+                ++S;
+            }
         }
     }
+    const int S_nb = S;
+    for (int s = 0; s < n_own; ++s) {
+        px_[S_nb + s] = disk[c * 3 * nm + perm[s]] + 0.0f;
+        py_[S_nb + s] = disk[c * 3 * nm + nm + perm[s]] + 0.0f;
+        pz_[S_nb + s] = disk[c * 3 * nm + 2 * nm + perm[s]] + 0.0f;
+    }
+    const int K = S_nb + n_own;
 
     /* cell centre (out_of_bound, subsweep.h:73-88): c*w - L/2 + w/2 in float */
-    const float Lx = (float)p->cps_x * p->w, Ly = (float)p->cps_y * p->w, Lz = (float)p->cps_z * p->w;
     const float hw = p->w / 2.0f;
     const float cxf = (float)x * p->w - Lx / 2.0f + hw;
     const float cyf = (float)y * p->w - Ly / 2.0f + hw;
     const float czf = (float)(p->z0 + zl) * p->w - Lz / 2.0f + hw;
 
+    double de_cell = 0.0;
     int i = 0;
     for (int m = 0; m < p->n_moves; ++m) {
         /* make_move (subsweep.h:60-71): p = x + normal*sigma */
@@ -219,48 +227,61 @@ static void subsweep_cell(const pmc_params* p, float* disk, const int16_t* n, in
         float g0, g1, g2;
         pmc_move_normals(wm, &g0, &g1, &g2);
         pmc_u32x4 wa = pmc_philox4x32_10((uint32_t)m, id, sweep, PMC_TAG_ACCEPT, k0, k1);
-        double T = pmc_accept_threshold(wa);
-        float xi = xs[i], yi = ys[i], zi = zs[i];
-        float px = xi + g0 * p->sigma;
-        float py = yi + g1 * p->sigma;
-        float pz = zi + g2 * p->sigma;
+        float T = pmc_accept_threshold(wa);
+        float xi = px_[S_nb + i], yi = py_[S_nb + i], zi = pz_[S_nb + i];
+        float qx = xi + g0 * p->sigma;
+        float qy = yi + g1 * p->sigma;
+        float qz = zi + g2 * p->sigma;
         ++*tri;
-        float ddx = px - cxf, ddy = py - cyf, ddz = pz - czf;
+        float ddx = qx - cxf, ddy = qy - cyf, ddz = qz - czf;
         int out = (ddx > hw) || (ddx < -hw) || (ddy > hw) || (ddy < -hw) || (ddz > hw) || (ddz < -hw);
         if (!out) {
             ++*ev;
-            /* energies (calculate_old/new_energy, subsweep.h:175-191): per-pair
-             * d_j = e_new - e_old, partner j accumulated on lane j%64 in ascending j, then
-             * the xor butterfly 1,2,4,8,16,32 of the wave reduction */
-            float lane[64];
-            for (int l = 0; l < 64; ++l) lane[l] = 0.0f;
-            for (int j = 0; j < S; ++j) {
-                if (j == i) continue;
-                float eo = pmc_lj_from_r2(pmc_r2(xi - xs[j], yi - ys[j], zi - zs[j]), rc2);
-                float en = pmc_lj_from_r2(pmc_r2(px - xs[j], py - ys[j], pz - zs[j]), rc2);
-                lane[j & 63] = lane[j & 63] + (en - eo);
+            /* energies (calculate_old/new_energy, subsweep.h:175-191).  Partner k (neighbours
+             * first, own cell after) runs on wave lane k%64, passes in ascending k.  Per lane:
+             * newp/oldp = neighbour new/old energy partials, down = own-cell (e_new - e_old);
+             * v = down + (newp - oldp); dE = xor butterfly 1,2,...,32 over the 64 lanes.
+             * (The kernel caches a particle's old partials after its first move; a recomputed
+             * old energy at the accepted position is bitwise its cached new energy, so the
+             * oracle simply recomputes.) */
+            float newp[64], oldp[64], down[64];
+            for (int l = 0; l < 64; ++l) { newp[l] = 0.0f; oldp[l] = 0.0f; down[l] = 0.0f; }
+            for (int k = 0; k < K; ++k) {
+                const int l = k & 63;
+                const float xj = px_[k], yj = py_[k], zj = pz_[k];
+                const float en = pmc_lj_from_r2(pmc_r2(qx - xj, qy - yj, qz - zj), rc2);
+                const float eo = pmc_lj_from_r2(pmc_r2(xi - xj, yi - yj, zi - zj), rc2);
+                if (k < S_nb) {
+                    newp[l] = newp[l] + en;
+                    oldp[l] = oldp[l] + eo;
+                } else if (k - S_nb != i) {
+                    down[l] = down[l] + (en - eo);
+                }
             }
+            float lane[64];
+            for (int l = 0; l < 64; ++l) lane[l] = down[l] + (newp[l] - oldp[l]);
             for (int mask = 1; mask < 64; mask <<= 1) {
                 float t[64];
                 for (int l = 0; l < 64; ++l) t[l] = lane[l] + lane[l ^ mask];
                 for (int l = 0; l < 64; ++l) lane[l] = t[l];
             }
-            float dE = lane[0];
+            const float dE = lane[0];
             /* accept_move (subsweep.h:209-216) as beta*dE < -log(u) */
-            if ((double)p->beta * (double)dE < T) {
-                xs[i] = px; ys[i] = py; zs[i] = pz;   /* cpy_proposed_to_D_sh :219-223 */
+            if ((double)p->beta * (double)dE < (double)T) {
+                px_[S_nb + i] = qx; py_[S_nb + i] = qy; pz_[S_nb + i] = qz;   /* :219-223 */
                 ++*acc;
-                *de += pmc_to_fixed((double)dE);
+                de_cell = de_cell + (double)dE;
             }
         }
         i += 1;
         if (i >= n_own) i = 0;
     }
+    *de += pmc_to_fixed(de_cell);
     /* cpy_D_sh_to_Disk (subsweep.h:29-36): write back in shuffled order */
     for (int s = 0; s < n_own; ++s) {
-        disk[c * 3 * nm + s] = xs[s];
-        disk[c * 3 * nm + nm + s] = ys[s];
-        disk[c * 3 * nm + 2 * nm + s] = zs[s];
+        disk[c * 3 * nm + s] = px_[S_nb + s];
+        disk[c * 3 * nm + nm + s] = py_[S_nb + s];
+        disk[c * 3 * nm + 2 * nm + s] = pz_[S_nb + s];
     }
 }
 
@@ -417,7 +438,8 @@ void orc_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
     pmc_u32x4 r = pmc_philox4x32_10(ctr[0], ctr[1], ctr[2], ctr[3], key[0], key[1]);
     for (int i = 0; i < 4; ++i) out[i] = r.v[i];
 }
-double orc_det_log(double x) { return pmc_det_log(x); }
+float orc_logf(float x) { return pmc_logf(x); }
+float orc_recip(float x) { return pmc_recip(x); }
 void orc_det_sincos_2pi(float u, float* s, float* c) { pmc_det_sincos_2pi(u, s, c); }
 void orc_move_normals(const uint32_t w[4], float g[3]) {
     pmc_u32x4 v;

@@ -49,7 +49,8 @@ int orc_run(const pmc_params* p, float* disk, int16_t* n, float* sdisk, int16_t*
 
 /* exported primitives for unit tests */
 void orc_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
-double orc_det_log(double x);
+float orc_logf(float x);
+float orc_recip(float x);
 void orc_det_sincos_2pi(float u, float* s, float* c);
 void orc_move_normals(const uint32_t w[4], float g[3]);
 float orc_pair_energy(float dx, float dy, float dz, float rc2);

@@ -79,8 +79,10 @@ def lib():
         L.orc_philox.argtypes = [C.POINTER(C.c_uint32 * 4), C.POINTER(C.c_uint32 * 2),
                                  C.POINTER(C.c_uint32 * 4)]
         L.orc_philox.restype = None
-        L.orc_det_log.argtypes = [C.c_double]
-        L.orc_det_log.restype = C.c_double
+        L.orc_logf.argtypes = [C.c_float]
+        L.orc_logf.restype = C.c_float
+        L.orc_recip.argtypes = [C.c_float]
+        L.orc_recip.restype = C.c_float
         L.orc_det_sincos_2pi.argtypes = [C.c_float, C.POINTER(C.c_float), C.POINTER(C.c_float)]
         L.orc_det_sincos_2pi.restype = None
         L.orc_move_normals.argtypes = [C.POINTER(C.c_uint32 * 4), C.POINTER(C.c_float * 3)]
@@ -192,8 +194,12 @@ def philox(ctr, key):
     return list(o)
 
 
-def det_log(x: float) -> float:
-    return lib().orc_det_log(x)
+def logf(x: float) -> float:
+    return lib().orc_logf(x)
+
+
+def recip(x: float) -> float:
+    return lib().orc_recip(x)
 
 
 def det_sincos_2pi(u: float):

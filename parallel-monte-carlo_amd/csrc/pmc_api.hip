@@ -75,7 +75,7 @@ int normalise(pmc_params* p) {
     if (p->z0 < 0 || p->z0 + p->nz_local > p->cps_z) return fail(PMC_ERR_ARG, "slab outside the box");
     if (!(p->w > 0.0f) || !(p->sigma >= 0.0f)) return fail(PMC_ERR_ARG, "w must be > 0, sigma >= 0");
     const int64_t cells = (int64_t)p->cps_x * p->cps_y * (p->nz_local + 2 * p->halo);
-    if (cells * 3 * p->nmax >= (int64_t)1 << 40) return fail(PMC_ERR_ARG, "box too large");
+    if (cells * 3 * p->nmax >= ((int64_t)1 << 32)) return fail(PMC_ERR_ARG, "box too large (2^32 coordinate slots per context)");
     if ((int64_t)p->cps_x * p->cps_y * p->cps_z > 0xFFFFFFFFll) return fail(PMC_ERR_ARG, "more than 2^32 cells");
     if (cells >= ((int64_t)1 << 31)) return fail(PMC_ERR_ARG, "more than 2^31 storage cells");
     return PMC_OK;
@@ -93,6 +93,10 @@ DevGeom make_geom(const pmc_params& p) {
     g.Ly = (float)p.cps_y * p.w;
     g.Lz = (float)p.cps_z * p.w;
     g.rc2 = pmc_cutoff_r2(p.w);
+    g.rc2f = pmc_filter_r2(g.rc2);
+    // a slot's old-energy partials are reused only if the slot moves again in the same visit:
+    // slot i < n_own with i + n_own < n_moves, hence i < n_moves / 2 (and < nmax)
+    g.ncache = p.n_moves / 2 < p.nmax ? p.n_moves / 2 : p.nmax;
     g.k0 = (uint32_t)p.seed;
     g.k1 = (uint32_t)(p.seed >> 32);
     return g;

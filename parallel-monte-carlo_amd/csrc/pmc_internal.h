@@ -18,7 +18,9 @@ constexpr int kStatCounters = 4;   // de_fixed, accepted, trials, evaluated
 struct DevGeom {
     int cps_x, cps_y, cps_z, nz_local, z0, halo, nmax, n_moves;
     int nslot;                     // power of two >= nmax (lanes per cell in shift/energy)
+    int ncache;                    // own slots with cached old-energy partials: min(nmax, n_moves)
     float w, beta, sigma, Lx, Ly, Lz, rc2;
+    float rc2f;                    // staging filter threshold (pmc_filter_r2)
     uint32_t k0, k1;
 };
 

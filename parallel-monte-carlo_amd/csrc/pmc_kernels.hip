@@ -29,15 +29,23 @@ __device__ __forceinline__ int as_i(float v) { return __builtin_bit_cast(int, v)
 // the same bits; the oracle replays exactly this tree (oracle/pmc_oracle.c subsweep_cell).
 // Mirror DPP patterns are used for the xor-4 / xor-8 steps: after the previous steps all lanes of
 // a quad (resp. half-row) hold equal values, so l^7 / l^15 supply the same operand as l^4 / l^8.
+// The xor-16 / xor-32 steps use gfx950's v_permlane16_swap / v_permlane32_swap: with both
+// operands = v the swapped pair holds (own, partner) and their sum is the butterfly step in every
+// lane (float add is commutative, so both lanes of a pair get identical bits).  No LDS, no SGPR.
 __device__ __forceinline__ float wave_sum_fixed_order(float v) {
     v = v + as_f(__builtin_amdgcn_mov_dpp(as_i(v), 0xB1, 0xF, 0xF, false));   // quad_perm 1,0,3,2
     v = v + as_f(__builtin_amdgcn_mov_dpp(as_i(v), 0x4E, 0xF, 0xF, false));   // quad_perm 2,3,0,1
     v = v + as_f(__builtin_amdgcn_mov_dpp(as_i(v), 0x141, 0xF, 0xF, false));  // row_half_mirror
     v = v + as_f(__builtin_amdgcn_mov_dpp(as_i(v), 0x140, 0xF, 0xF, false));  // row_mirror
-    v = v + as_f(__builtin_amdgcn_ds_swizzle(as_i(v), 0x401F));               // xor 16 (in 32)
-    float a = as_f(__builtin_amdgcn_readlane(as_i(v), 0));
-    float b = as_f(__builtin_amdgcn_readlane(as_i(v), 32));
-    return a + b;                                                             // xor 32
+    {
+        const auto r = __builtin_amdgcn_permlane16_swap((unsigned)as_i(v), (unsigned)as_i(v), false, false);
+        v = as_f((int)r[0]) + as_f((int)r[1]);                                // xor 16
+    }
+    {
+        const auto r = __builtin_amdgcn_permlane32_swap((unsigned)as_i(v), (unsigned)as_i(v), false, false);
+        v = as_f((int)r[0]) + as_f((int)r[1]);                                // xor 32
+    }
+    return v;
 }
 
 __device__ __forceinline__ int wave_uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -49,165 +57,244 @@ __device__ __forceinline__ int64_t sidx(const DevGeom& g, int x, int y, int zl) 
 
 // ------------------------------------------------------------------------------------------
 // subsweep: one colour phase, one wave per cell (subsweep_kernel, subsweep.h:240-300)
+//
+// Per cell visit (one wave):
+//   1. stencil table: lane k < 27 computes stencil cell k's storage offset and periodic image
+//      and loads its count; every global load of the visit is issued at once (counts, the 26
+//      neighbours' full rows -- a 64 B row sits inside one 128 B line, so the unused slots cost
+//      no extra lines -- and the own rows): one HBM round trip per visit;
+//   2. RNG while the loads fly, ONE Philox call per lane: lanes 0-15 trial moves, 16-31
+//      acceptance thresholds, 32-63 Fisher-Yates words; then one log + one sincos per lane
+//      (lanes 0-15 Box-Muller pair A, 32-47 pair B with words swizzled in, 16-31 -log u);
+//   3. stage the neighbours into LDS, keeping (ballot + mbcnt compaction) only partners within
+//      the cutoff of the own cell's box -- the others contribute exactly 0 -- then the own cell
+//      (shuffled) after them;
+//   4. n_M moves: lane l evaluates partners k = l + 64*pass; a particle's neighbour old-energy
+//      partials are kept per lane in LDS after its first move (neighbours are static in a phase
+//      and a recomputation would give the same bits), so later moves evaluate only new energies;
+//      one fixed-order DPP/permlane reduction gives dE; accept in-kernel, wave-uniformly;
+//   5. write back the own cell; one atomic per counter per wave.
+// LDS per wave: 3 * 27*nmax floats (partners) + 64 * ncache floats (old-energy partials).
 // ------------------------------------------------------------------------------------------
-template <int NSLOT>
+template <int NSLOT, int NMC>
 __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep(DevGeom g, float* __restrict__ disk,
                                                                   const int16_t* __restrict__ ncnt,
                                                                   int ox, int oy, int oz, uint32_t sweep,
                                                                   unsigned long long* __restrict__ stats) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int CPP = kWave / NSLOT;            // stencil cells staged per pass
+    constexpr int NP = (26 + CPP - 1) / CPP;      // staging passes over the 26 neighbours
     const int lane = threadIdx.x & (kWave - 1);
     const int wv = threadIdx.x >> 6;
-    const int nm = g.nmax;
+    const int nm = NMC > 0 ? NMC : g.nmax;        // compile-time for the common nmax
     const int cap = 27 * nm;
-    float* xs = smem + wv * 3 * cap;
-    float* ys = xs + cap;
-    float* zs = ys + cap;
+    float* px_ = smem + wv * (3 * cap + kWave * g.ncache);
+    float* py_ = px_ + cap;
+    float* pz_ = py_ + cap;
+    float* cache = pz_ + cap;
 
     // XCD-aware block order: blocks b and b+8 share an XCD (round-robin dispatch), so give each
     // XCD a contiguous run of cells -> neighbouring stencils share that XCD's L2.  Speed only.
     uint32_t nblk = gridDim.x, b = blockIdx.x;
     if ((nblk & 7u) == 0u) b = (b & 7u) * (nblk >> 3) + (b >> 3);
     const int ncx = g.cps_x >> 1, ncy = g.cps_y >> 1, ncz = g.nz_local >> 1;
-    const int64_t total = (int64_t)ncx * ncy * ncz;
-    const int64_t t = (int64_t)b * kSubWaves + wv;
+    const int total = ncx * ncy * ncz;
+    const int t = (int)b * kSubWaves + wv;
     if (t >= total) return;
-    const int ta = wave_uniform((int)(t % ncx));
-    const int tb = wave_uniform((int)((t / ncx) % ncy));
-    const int tc = wave_uniform((int)(t / ((int64_t)ncx * ncy)));
+    const int ta = wave_uniform(t % ncx);
+    const int tb = wave_uniform((t / ncx) % ncy);
+    const int tc = wave_uniform(t / (ncx * ncy));
     const int x = 2 * ta + ox, y = 2 * tb + oy, zl = 2 * tc + oz;
-    const int64_t c = sidx(g, x, y, zl);
-    const int n_own = wave_uniform(ncnt[c]);
-    if (n_own == 0) return;                                   // subsweep.h:252-253
-    const uint32_t id = (uint32_t)x + (uint32_t)g.cps_x * ((uint32_t)y + (uint32_t)g.cps_y * (uint32_t)(g.z0 + zl));
+    const int zg0 = g.z0 + zl;
+    const int plane = g.cps_x * g.cps_y;
+    const uint32_t c = (uint32_t)(x + g.cps_x * y + plane * (zl + g.halo));
+    const uint32_t id = (uint32_t)x + (uint32_t)g.cps_x * ((uint32_t)y + (uint32_t)g.cps_y * (uint32_t)zg0);
+    const uint32_t k0 = g.k0, k1 = g.k1;
 
-    // ---- stencil table: lane k < 27 describes stencil cell k ------------------------------
-    int k_cnt = 0, k_idx = 0;
+    // ---- 1. stencil table (lane k < 27) and all global loads ------------------------------------
+    uint32_t k_off = c * (uint32_t)(3 * nm);      // element offset of the cell's rows
     float k_sx = 0.0f, k_sy = 0.0f, k_sz = 0.0f;
     if (lane < 27) {
         const int hx = lane / 9, hy = (lane / 3) % 3, hz = lane % 3;   // {0,-1,+1} order
-        const int dx = hx == 0 ? 0 : (hx == 1 ? -1 : 1);
-        const int dy = hy == 0 ? 0 : (hy == 1 ? -1 : 1);
+        int nx = x + (hx == 0 ? 0 : (hx == 1 ? -1 : 1));
+        int ny = y + (hy == 0 ? 0 : (hy == 1 ? -1 : 1));
         const int dz = hz == 0 ? 0 : (hz == 1 ? -1 : 1);
-        int nx = x + dx, ny = y + dy;
         if (nx < 0) { nx += g.cps_x; k_sx = -g.Lx; } else if (nx >= g.cps_x) { nx -= g.cps_x; k_sx = g.Lx; }
         if (ny < 0) { ny += g.cps_y; k_sy = -g.Ly; } else if (ny >= g.cps_y) { ny -= g.cps_y; k_sy = g.Ly; }
-        const int zg = g.z0 + zl + dz;
-        if (zg < 0) k_sz = -g.Lz; else if (zg >= g.cps_z) k_sz = g.Lz;
-        const int nzl = g.halo ? zl + dz : (zl + dz + g.cps_z) % g.cps_z;
-        k_idx = (int)sidx(g, nx, ny, nzl);
-        k_cnt = ncnt[k_idx];
+        const int zgn = zg0 + dz;
+        if (zgn < 0) k_sz = -g.Lz; else if (zgn >= g.cps_z) k_sz = g.Lz;
+        int nzl = zl + dz;
+        if (!g.halo) nzl = nzl < 0 ? nzl + g.cps_z : (nzl >= g.cps_z ? nzl - g.cps_z : nzl);
+        k_off = (uint32_t)(nx + g.cps_x * ny + plane * (nzl + g.halo)) * (uint32_t)(3 * nm);
     }
-    // inclusive scan of counts -> staged base of each stencil cell
-    int incl = k_cnt;
+    const int k_cnt = ncnt[k_off / (uint32_t)(3 * nm)];
+    const int p = lane & (NSLOT - 1);
+    const int kk = lane / NSLOT;
+    const int pp = p < nm ? p : 0;
+    float vx[NP], vy[NP], vz[NP];
 #pragma unroll
-    for (int o = 1; o < 32; o <<= 1) {
-        int v = __shfl_up(incl, o);
-        if (lane >= o) incl += v;
+    for (int q = 0; q < NP; ++q) {
+        const int k = 1 + q * CPP + kk;
+        const uint32_t off = (uint32_t)__shfl((int)k_off, k < 27 ? k : 26) + (uint32_t)pp;
+        vx[q] = disk[off];
+        vy[q] = disk[off + nm];
+        vz[q] = disk[off + 2 * nm];
     }
-    const int S = __builtin_amdgcn_readlane(incl, 26);        // staged partners incl. own cell
-    const int k_base = incl - k_cnt;
+    float ownx, owny, ownz;
+    {
+        const uint32_t off = c * (uint32_t)(3 * nm) + (uint32_t)(lane < nm ? lane : 0);
+        ownx = disk[off];
+        owny = disk[off + nm];
+        ownz = disk[off + 2 * nm];
+    }
 
-    const uint32_t k0 = g.k0, k1 = g.k1;
+    // ---- 2. random numbers for the first 16 moves + the shuffle (overlaps the loads) ------------
+    float G0 = 0.0f, G1 = 0.0f, TT = 0.0f;
+    int jv = 0;
+    auto rng_chunk = [&](int m0, bool first) {
+        uint32_t idx, tag;
+        if (lane < 16) { idx = (uint32_t)(m0 + lane); tag = PMC_TAG_MOVE; }
+        else if (lane < 32) { idx = (uint32_t)(m0 + lane - 16); tag = PMC_TAG_ACCEPT; }
+        else { idx = (uint32_t)(lane - 32); tag = PMC_TAG_SHUFFLE; }
+        const pmc_u32x4 w = pmc_philox4x32_10(idx, id, sweep, tag, k0, k1);
+        if (first) {
+            const int jraw = (int)pmc_bounded(w.v[0], (uint32_t)(lane - 32 + 1));
+            jv = __shfl(jraw, (lane + 32) & 63);                  // slot i's FY index in lane i
+        }
+        const uint32_t b2 = (uint32_t)__shfl((int)w.v[2], lane & 15);
+        const uint32_t b3 = (uint32_t)__shfl((int)w.v[3], lane & 15);
+        const uint32_t wl = lane < 32 ? w.v[0] : b2;
+        const uint32_t ws = lane < 32 ? w.v[1] : b3;
+        const float lg = pmc_logf(pmc_u01(wl));
+        const float R = __builtin_sqrtf(-2.0f * lg);
+        float sn, cs;
+        pmc_det_sincos_2pi(pmc_u01(ws), &sn, &cs);
+        G0 = R * cs;      // lanes 0-15: g0 of move m0+lane; lanes 32-47: g2 of move m0+lane-32
+        G1 = R * sn;      // lanes 0-15: g1
+        TT = -lg;         // lanes 16-31: acceptance threshold of move m0+lane-16
+    };
+    rng_chunk(0, true);
 
-    // ---- Fisher-Yates shuffle of the own cell (random_shuffle, subsweep.h:50-58; fixes R1) ----
+    const int n_own = __builtin_amdgcn_readfirstlane(k_cnt);   // lane 0 = own cell
+    if (n_own == 0) return;                                     // subsweep.h:252-253
+    if (n_own > 32) {     // nmax > 32: Fisher-Yates words of slots 32..63
+        const pmc_u32x4 w = pmc_philox4x32_10((uint32_t)lane, id, sweep, PMC_TAG_SHUFFLE, k0, k1);
+        if (lane >= 32) jv = (int)pmc_bounded(w.v[0], (uint32_t)(lane + 1));
+    }
+
+    // ---- Fisher-Yates shuffle of the own cell (random_shuffle, subsweep.h:50-58; fixes R1) ---
     int perm = lane;
-    {
-        int jv = 0;
-        if (lane >= 1 && lane < n_own) {
-            pmc_u32x4 wv4 = pmc_philox4x32_10((uint32_t)lane, id, sweep, PMC_TAG_SHUFFLE, k0, k1);
-            jv = (int)pmc_bounded(wv4.v[0], (uint32_t)(lane + 1));
-        }
-        for (int i = n_own - 1; i > 0; --i) {
-            const int j = __builtin_amdgcn_readlane(jv, i);
-            const int vi = __builtin_amdgcn_readlane(perm, i);
-            const int vj = __builtin_amdgcn_readlane(perm, j);
-            perm = lane == i ? vj : (lane == j ? vi : perm);
-        }
+    for (int i = n_own - 1; i > 0; --i) {
+        const int j = __builtin_amdgcn_readlane(jv, i);
+        const int vi = __builtin_amdgcn_readlane(perm, i);
+        const int vj = __builtin_amdgcn_readlane(perm, j);
+        perm = lane == i ? vj : (lane == j ? vi : perm);
     }
 
-    // ---- stage the 27-cell stencil into LDS (cpy_to_Dsh, subsweep.h:18-27; kernel.cu:269-278) --
+    // ---- 3. stage neighbours (filtered, compacted) then the own cell -------------------------
+    float blo[3], bhi[3];
+    pmc_cell_box(x, y, zg0, g.w, g.Lx, g.Ly, g.Lz, blo, bhi);
+    int S_nb = 0;
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+        const int k = 1 + q * CPP + kk;
+        const int ks = k < 27 ? k : 26;
+        const int cnt = __shfl(k_cnt, ks);
+        // periodic image of stencil cell k (apply_PBC, subsweep.h:139-151, per staged cell)
+        const float ux = vx[q] + __shfl(k_sx, ks);
+        const float uy = vy[q] + __shfl(k_sy, ks);
+        const float uz = vz[q] + __shfl(k_sz, ks);
+        const bool keep = (k < 27) && (p < cnt) && (pmc_box_d2(ux, uy, uz, blo, bhi) <= g.rc2f);
+        const unsigned long long mk = __ballot(keep);
+        if (keep) {
+            const int dst = S_nb + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
+                                               __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+            px_[dst] = ux;
+            py_[dst] = uy;
+            pz_[dst] = uz;
+        }
+        S_nb += __popcll(mk);
+    }
     {
-        const int p = lane & (NSLOT - 1);
-        const int kk = lane / NSLOT;
-        for (int q = 0; q < (27 + CPP - 1) / CPP; ++q) {
-            const int k = q * CPP + kk;
-            const int ks = k < 27 ? k : 26;
-            const int cnt = __shfl(k_cnt, ks);
-            const int base = __shfl(k_base, ks);
-            const int idx = __shfl(k_idx, ks);
-            const float sx = __shfl(k_sx, ks), sy = __shfl(k_sy, ks), sz = __shfl(k_sz, ks);
-            if (k < 27 && p < cnt) {
-                const int src = (k == 0) ? perm : p;          // k==0 only in lanes 0..NSLOT-1
-                const float* cell = disk + (int64_t)idx * 3 * nm;
-                const float vx = cell[src] + sx;
-                const float vy = cell[nm + src] + sy;
-                const float vz = cell[2 * nm + src] + sz;
-                xs[base + p] = vx;
-                ys[base + p] = vy;
-                zs[base + p] = vz;
-            }
+        const float sxo = as_f(__shfl(as_i(ownx), perm));
+        const float syo = as_f(__shfl(as_i(owny), perm));
+        const float szo = as_f(__shfl(as_i(ownz), perm));
+        if (lane < n_own) {
+            px_[S_nb + lane] = sxo + 0.0f;
+            py_[S_nb + lane] = syo + 0.0f;
+            pz_[S_nb + lane] = szo + 0.0f;
         }
     }
+    const int K = S_nb + n_own;
 
     // cell centre for out_of_bound (subsweep.h:73-88): c*w - L/2 + w/2 in float
     const float hw = g.w / 2.0f;
     const float cxf = (float)x * g.w - g.Lx / 2.0f + hw;
     const float cyf = (float)y * g.w - g.Ly / 2.0f + hw;
-    const float czf = (float)(g.z0 + zl) * g.w - g.Lz / 2.0f + hw;
+    const float czf = (float)zg0 * g.w - g.Lz / 2.0f + hw;
     const double beta_d = (double)g.beta;
+    const float rc2 = g.rc2;
+    const int ncache = g.ncache;
 
-    int64_t de_fix = 0;
+    uint64_t cvalid = 0;
+    double de_cell = 0.0;
     int n_acc = 0, n_ev = 0;
     int i = 0;
-    for (int m0 = 0; m0 < g.n_moves; m0 += kWave) {
-        // per-move random numbers, one move per lane (make_move's curand_normal x3 and
-        // accept_move's curand_uniform, subsweep.h:60-71,212)
-        float G0 = 0.0f, G1 = 0.0f, G2 = 0.0f;
-        double T = 0.0;
-        const int mm = m0 + lane;
-        if (mm < g.n_moves) {
-            pmc_u32x4 wm = pmc_philox4x32_10((uint32_t)mm, id, sweep, PMC_TAG_MOVE, k0, k1);
-            pmc_move_normals(wm, &G0, &G1, &G2);
-            pmc_u32x4 wa = pmc_philox4x32_10((uint32_t)mm, id, sweep, PMC_TAG_ACCEPT, k0, k1);
-            T = pmc_accept_threshold(wa);
-        }
-        const uint64_t Tb = __builtin_bit_cast(uint64_t, T);
-        const int Tlo = (int)(uint32_t)Tb, Thi = (int)(uint32_t)(Tb >> 32);
-        const int mend = (g.n_moves - m0) < kWave ? (g.n_moves - m0) : kWave;
+    // ---- 4. trial moves --------------------------------------------------------------------
+    for (int m0 = 0; m0 < g.n_moves; m0 += 16) {
+        if (m0 > 0) rng_chunk(m0, false);
+        const int mend = (g.n_moves - m0) < 16 ? (g.n_moves - m0) : 16;
         for (int ml = 0; ml < mend; ++ml) {
             const float g0 = as_f(__builtin_amdgcn_readlane(as_i(G0), ml));
             const float g1 = as_f(__builtin_amdgcn_readlane(as_i(G1), ml));
-            const float g2 = as_f(__builtin_amdgcn_readlane(as_i(G2), ml));
-            const uint32_t tl = (uint32_t)__builtin_amdgcn_readlane(Tlo, ml);
-            const uint32_t th = (uint32_t)__builtin_amdgcn_readlane(Thi, ml);
-            const double Tm = __builtin_bit_cast(double, ((uint64_t)th << 32) | tl);
-            const float xi = xs[i], yi = ys[i], zi = zs[i];
-            const float px = xi + g0 * g.sigma;
-            const float py = yi + g1 * g.sigma;
-            const float pz = zi + g2 * g.sigma;
-            const float ddx = px - cxf, ddy = py - cyf, ddz = pz - czf;
+            const float g2 = as_f(__builtin_amdgcn_readlane(as_i(G0), 32 + ml));
+            const float Tm = as_f(__builtin_amdgcn_readlane(as_i(TT), 16 + ml));
+            const int si = S_nb + i;
+            const float xi = px_[si], yi = py_[si], zi = pz_[si];
+            const float qx = xi + g0 * g.sigma;
+            const float qy = yi + g1 * g.sigma;
+            const float qz = zi + g2 * g.sigma;
+            const float ddx = qx - cxf, ddy = qy - cyf, ddz = qz - czf;
             const bool out = (ddx > hw) || (ddx < -hw) || (ddy > hw) || (ddy < -hw) || (ddz > hw) ||
                              (ddz < -hw);
             if (!out) {
                 ++n_ev;
-                float acc = 0.0f;
-                for (int j0 = 0; j0 < S; j0 += kWave) {
-                    const int j = j0 + lane;
-                    const bool valid = (j < S) && (j != i);
-                    const int jr = j < S ? j : 0;
-                    const float xj = xs[jr], yj = ys[jr], zj = zs[jr];
-                    const float eo = pmc_lj_from_r2(pmc_r2(xi - xj, yi - yj, zi - zj), g.rc2);
-                    const float en = pmc_lj_from_r2(pmc_r2(px - xj, py - yj, pz - zj), g.rc2);
-                    const float dd = en - eo;
-                    acc = acc + (valid ? dd : 0.0f);
+                const bool cached = (cvalid >> i) & 1ull;
+                float newp = 0.0f, oldp = 0.0f, down = 0.0f;
+                int k0p = 0;
+                if (cached) {
+                    // neighbour-only passes: new energies only
+                    for (; k0p + kWave <= S_nb; k0p += kWave) {
+                        const int k = k0p + lane;
+                        const float xj = px_[k], yj = py_[k], zj = pz_[k];
+                        newp = newp + pmc_lj_from_r2(pmc_r2(qx - xj, qy - yj, qz - zj), rc2);
+                    }
                 }
-                const float dE = wave_sum_fixed_order(acc);
-                if (beta_d * (double)dE < Tm) {                 // accept_move, subsweep.h:209-216
-                    if (lane == 0) { xs[i] = px; ys[i] = py; zs[i] = pz; }
+                for (; k0p < K; k0p += kWave) {
+                    const int k = k0p + lane;
+                    const int kr = k < K ? k : 0;
+                    const float xj = px_[kr], yj = py_[kr], zj = pz_[kr];
+                    const float en = pmc_lj_from_r2(pmc_r2(qx - xj, qy - yj, qz - zj), rc2);
+                    const float eo = pmc_lj_from_r2(pmc_r2(xi - xj, yi - yj, zi - zj), rc2);
+                    const bool is_nb = k < S_nb;
+                    const bool is_own = (k >= S_nb) && (k < K) && (k - S_nb != i);
+                    newp = newp + (is_nb ? en : 0.0f);
+                    oldp = oldp + ((is_nb && !cached) ? eo : 0.0f);
+                    down = down + (is_own ? (en - eo) : 0.0f);
+                }
+                if (cached) oldp = cache[i * kWave + lane];
+                const float v = down + (newp - oldp);
+                const float dE = wave_sum_fixed_order(v);
+                const bool accept = beta_d * (double)dE < (double)Tm;   // accept_move, subsweep.h:209-216
+                // keep the partials only if slot i moves again in this visit and fits the cache
+                if (i < ncache && (accept || !cached)) {
+                    cache[i * kWave + lane] = accept ? newp : oldp;
+                    cvalid |= 1ull << i;
+                }
+                if (accept) {
+                    if (lane == 0) { px_[si] = qx; py_[si] = qy; pz_[si] = qz; }
                     ++n_acc;
-                    de_fix += pmc_to_fixed((double)dE);
+                    de_cell = de_cell + (double)dE;
                 }
             }
             i += 1;
@@ -215,16 +302,16 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep(DevGeom g, float
         }
     }
 
-    // ---- write back the own cell in shuffled order (cpy_D_sh_to_Disk, subsweep.h:29-36) ----
+    // ---- 5. write back the own cell in shuffled order (cpy_D_sh_to_Disk, subsweep.h:29-36) ----
     if (lane < n_own) {
-        float* cell = disk + c * 3 * nm;
-        cell[lane] = xs[lane];
-        cell[nm + lane] = ys[lane];
-        cell[2 * nm + lane] = zs[lane];
+        const uint32_t off = c * (uint32_t)(3 * nm) + (uint32_t)lane;
+        disk[off] = px_[S_nb + lane];
+        disk[off + nm] = py_[S_nb + lane];
+        disk[off + 2 * nm] = pz_[S_nb + lane];
     }
     if (lane == 0) {
-        const int slot = (int)(t & (kStatSlots - 1));
-        atomicAdd(&stats[0 * kStatSlots + slot], (unsigned long long)de_fix);
+        const int slot = t & (kStatSlots - 1);
+        atomicAdd(&stats[0 * kStatSlots + slot], (unsigned long long)pmc_to_fixed(de_cell));
         atomicAdd(&stats[1 * kStatSlots + slot], (unsigned long long)n_acc);
         atomicAdd(&stats[2 * kStatSlots + slot], (unsigned long long)g.n_moves);
         atomicAdd(&stats[3 * kStatSlots + slot], (unsigned long long)n_ev);
@@ -458,7 +545,7 @@ __global__ void k_selftest(const uint32_t* __restrict__ words, int count, float*
     out_f[4 * i + 1] = g1;
     out_f[4 * i + 2] = g2;
     out_f[4 * i + 3] = pmc_lj_from_r2(pmc_r2(dx, dy, dz), rc2);
-    out_d[2 * i + 0] = pmc_accept_threshold(w);
+    out_d[2 * i + 0] = (double)pmc_accept_threshold(w);
     out_d[2 * i + 1] = (double)pmc_to_fixed((double)out_f[4 * i + 3]);
 }
 
@@ -471,13 +558,19 @@ hipError_t launch_subsweep(const DevGeom& g, float* disk, const int16_t* n, int 
                            uint32_t sweep, unsigned long long* stats, hipStream_t st) {
     const int64_t total = (int64_t)(g.cps_x / 2) * (g.cps_y / 2) * (g.nz_local / 2);
     const int64_t blocks = (total + kSubWaves - 1) / kSubWaves;
-    const size_t lds = sizeof(float) * 3 * 27 * (size_t)g.nmax * kSubWaves;
+    const size_t lds = sizeof(float) * (3 * 27 * (size_t)g.nmax + kWave * (size_t)g.ncache) * kSubWaves;
     dim3 grid((unsigned)blocks), block(kWave * kSubWaves);
-    switch (g.nslot) {
-        case 8: hipLaunchKernelGGL(k_subsweep<8>, grid, block, lds, st, g, disk, n, ox, oy, oz, sweep, stats); break;
-        case 16: hipLaunchKernelGGL(k_subsweep<16>, grid, block, lds, st, g, disk, n, ox, oy, oz, sweep, stats); break;
-        case 32: hipLaunchKernelGGL(k_subsweep<32>, grid, block, lds, st, g, disk, n, ox, oy, oz, sweep, stats); break;
-        default: hipLaunchKernelGGL(k_subsweep<64>, grid, block, lds, st, g, disk, n, ox, oy, oz, sweep, stats); break;
+    if (g.nmax == 16) {
+        hipLaunchKernelGGL((k_subsweep<16, 16>), grid, block, lds, st, g, disk, n, ox, oy, oz, sweep, stats);
+    } else if (g.nmax == 32) {
+        hipLaunchKernelGGL((k_subsweep<32, 32>), grid, block, lds, st, g, disk, n, ox, oy, oz, sweep, stats);
+    } else {
+        switch (g.nslot) {
+            case 8: hipLaunchKernelGGL((k_subsweep<8, 0>), grid, block, lds, st, g, disk, n, ox, oy, oz, sweep, stats); break;
+            case 16: hipLaunchKernelGGL((k_subsweep<16, 0>), grid, block, lds, st, g, disk, n, ox, oy, oz, sweep, stats); break;
+            case 32: hipLaunchKernelGGL((k_subsweep<32, 0>), grid, block, lds, st, g, disk, n, ox, oy, oz, sweep, stats); break;
+            default: hipLaunchKernelGGL((k_subsweep<64, 0>), grid, block, lds, st, g, disk, n, ox, oy, oz, sweep, stats); break;
+        }
     }
     return hipGetLastError();
 }

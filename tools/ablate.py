@@ -1,0 +1,30 @@
+"""Time one colour phase of the subsweep at 128^3/1e7 for several n_moves (ablation)."""
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "parallel-monte-carlo_amd"))
+import torch  # noqa: E402,F401
+import pmc_amd  # noqa: E402
+
+cps = int(os.environ.get("CPS", "128"))
+atoms = int(os.environ.get("ATOMS", "10000000"))
+for nm in [int(v) for v in os.environ.get("MOVES", "0,1,5,10,20").split(",")]:
+    ctx = pmc_amd.PmcContext(cps, n_moves=nm)
+    ctx.init_lattice(atoms)
+    # equilibrate a little with the standard chain so the state is not the lattice
+    ctx.synchronize()
+    for s in range(2):
+        ctx.sweep(s)
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    reps = 5
+    for s in range(reps):
+        for c in range(8):
+            ctx.phase(c, 100 + s)
+    ctx.synchronize()
+    dt = (time.perf_counter() - t0) / (reps * 8)
+    st = ctx.stats()
+    print(f"n_moves={nm:3d}  phase_ms={dt*1e3:.4f}  evaluated/trials={st['evaluated']/max(1,st['trials']):.3f}", flush=True)
+    ctx.close()
