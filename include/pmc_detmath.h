@@ -177,13 +177,18 @@ PMC_HD float pmc_recip(float x) {
     return y;
 }
 
-PMC_HD float pmc_lj_from_r2(float r2, float rc2) {
-    float rr = r2 < PMC_R2_MIN ? PMC_R2_MIN : r2;
+/* Quarter pair energy u = r^-12 - r^-6 (e = 4u).  Scaling by 4 is exact in binary floating
+ * point, so sums of 4u equal 4 * (sums of u) bit for bit: the kernels accumulate u and apply the
+ * factor 4 once per lane. */
+PMC_HD float pmc_lj4_from_r2(float r2, float rc2) {
+    float rr = __builtin_fmaxf(r2, PMC_R2_MIN);
     float inv = pmc_recip(rr);
     float p6 = inv * inv * inv;
-    float e = 4.0f * (p6 * p6 - p6);
-    return r2 <= rc2 ? e : 0.0f;
+    float u = p6 * p6 - p6;
+    return r2 <= rc2 ? u : 0.0f;
 }
+
+PMC_HD float pmc_lj_from_r2(float r2, float rc2) { return 4.0f * pmc_lj4_from_r2(r2, rc2); }
 
 /* Conservative partner filter (staging): squared distance from a staged partner to the own
  * cell's closed box [lo, hi] (each side padded by PMC_BOX_PAD).  A partner with

@@ -27,6 +27,7 @@ struct pmc_ctx {
     unsigned long long* stats = nullptr;   // kStatCounters * kStatSlots
     unsigned long long* eacc = nullptr;    // kStatSlots (energy)
     uint32_t* flags = nullptr;
+    int* ovf = nullptr;                    // subsweep overflow queue (1 + cells per colour)
     int32_t* tmp_cnt = nullptr;
     int32_t* tmp_idx = nullptr;
     float* d_r = nullptr;
@@ -136,7 +137,7 @@ int enqueue_sweep(pmc_ctx* c, uint32_t sweep) {
         int o[3];
         pmc_colour_offset(plan.order[k], o);
         hipError_t e = launch_subsweep(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep,
-                                       c->stats, c->stream);
+                                       c->stats, c->ovf, c->stream);
         if (e != hipSuccess) return hip_fail(e, "subsweep launch");
     }
     hipError_t e = launch_shift(c->G, c->disk[c->cur], c->n[c->cur], c->disk[c->cur ^ 1], c->n[c->cur ^ 1],
@@ -182,6 +183,11 @@ int pmc_create(const pmc_params* params, pmc_ctx** out) {
     if ((e = hipMalloc(&c->eacc, sizeof(unsigned long long) * kStatSlots)) != hipSuccess)
         return cleanup(hip_fail(e, "hipMalloc eacc"));
     if ((e = hipMalloc(&c->flags, 16)) != hipSuccess) return cleanup(hip_fail(e, "hipMalloc flags"));
+    {
+        const size_t per_colour = (size_t)(p.cps_x / 2) * (p.cps_y / 2) * (p.nz_local / 2);
+        if ((e = hipMalloc(&c->ovf, sizeof(int) * (1 + per_colour))) != hipSuccess)
+            return cleanup(hip_fail(e, "hipMalloc ovf"));
+    }
     if ((e = hipMemset(c->flags, 0, 16)) != hipSuccess) return cleanup(hip_fail(e, "hipMemset"));
     if ((e = hipEventCreate(&c->ev0)) != hipSuccess) return cleanup(hip_fail(e, "hipEventCreate"));
     if ((e = hipEventCreate(&c->ev1)) != hipSuccess) return cleanup(hip_fail(e, "hipEventCreate"));
@@ -197,6 +203,7 @@ void pmc_destroy(pmc_ctx* c) {
     if (c->stats) (void)hipFree(c->stats);
     if (c->eacc) (void)hipFree(c->eacc);
     if (c->flags) (void)hipFree(c->flags);
+    if (c->ovf) (void)hipFree(c->ovf);
     if (c->tmp_cnt) (void)hipFree(c->tmp_cnt);
     if (c->tmp_idx) (void)hipFree(c->tmp_idx);
     if (c->d_r) (void)hipFree(c->d_r);
@@ -263,7 +270,8 @@ int pmc_subsweep(pmc_ctx* c, float* d_disk, const int16_t* d_n, const int offset
     if (!c || !d_disk || !d_n || !offset) return fail(PMC_ERR_ARG, "bad argument");
     for (int k = 0; k < 3; ++k)
         if (offset[k] != 0 && offset[k] != 1) return fail(PMC_ERR_ARG, "offset must be in {0,1}^3");
-    hipError_t e = launch_subsweep(c->G, d_disk, d_n, offset[0], offset[1], offset[2], sweep, c->stats, c->stream);
+    hipError_t e = launch_subsweep(c->G, d_disk, d_n, offset[0], offset[1], offset[2], sweep, c->stats, c->ovf,
+                                   c->stream);
     return e == hipSuccess ? PMC_OK : hip_fail(e, "subsweep launch");
 }
 

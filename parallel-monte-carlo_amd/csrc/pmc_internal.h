@@ -25,8 +25,10 @@ struct DevGeom {
 };
 
 // Launchers (pmc_kernels.hip).  All asynchronous on `st`.
+// ovf: int[1 + cells_per_colour] scratch (overflow queue for the full-capacity fallback)
 hipError_t launch_subsweep(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
-                           uint32_t sweep, unsigned long long* stats, hipStream_t st);
+                           uint32_t sweep, unsigned long long* stats, int* ovf, hipStream_t st);
+int subsweep_capacity(const DevGeom& g);
 hipError_t launch_shift(const DevGeom& g, const float* din, const int16_t* nin, float* dout,
                         int16_t* nout, int f, float d, uint32_t* flags, hipStream_t st);
 hipError_t launch_init_r(const DevGeom& g, int64_t n_atoms, int64_t n_cube, float* r, hipStream_t st);

@@ -15,6 +15,8 @@
 //
 // Build with -ffp-contract=off: every float/double op must stay a single IEEE op (the oracle,
 // compiled by gcc with the same flag, reproduces the results bit for bit).
+#include <cstdlib>
+
 #include "pmc_internal.h"
 #include "../../include/pmc_detmath.h"
 
@@ -76,31 +78,21 @@ __device__ __forceinline__ int64_t sidx(const DevGeom& g, int x, int y, int zl) 
 //   5. write back the own cell; one atomic per counter per wave.
 // LDS per wave: 3 * 27*nmax floats (partners) + 64 * ncache floats (old-energy partials).
 // ------------------------------------------------------------------------------------------
+// Returns false (and leaves the cell untouched) when the cell's staged partners do not fit the
+// LDS capacity `cap`; the caller queues it for the full-capacity fallback launch.
 template <int NSLOT, int NMC>
-__global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep(DevGeom g, float* __restrict__ disk,
-                                                                  const int16_t* __restrict__ ncnt,
-                                                                  int ox, int oy, int oz, uint32_t sweep,
-                                                                  unsigned long long* __restrict__ stats) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
+__device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restrict__ disk,
+                                              const int16_t* __restrict__ ncnt, int ox, int oy, int oz,
+                                              uint32_t sweep, unsigned long long* __restrict__ stats,
+                                              float* __restrict__ px_, int cap, int t) {
     constexpr int CPP = kWave / NSLOT;            // stencil cells staged per pass
     constexpr int NP = (26 + CPP - 1) / CPP;      // staging passes over the 26 neighbours
     const int lane = threadIdx.x & (kWave - 1);
-    const int wv = threadIdx.x >> 6;
     const int nm = NMC > 0 ? NMC : g.nmax;        // compile-time for the common nmax
-    const int cap = 27 * nm;
-    float* px_ = smem + wv * (3 * cap + kWave * g.ncache);
     float* py_ = px_ + cap;
     float* pz_ = py_ + cap;
     float* cache = pz_ + cap;
-
-    // XCD-aware block order: blocks b and b+8 share an XCD (round-robin dispatch), so give each
-    // XCD a contiguous run of cells -> neighbouring stencils share that XCD's L2.  Speed only.
-    uint32_t nblk = gridDim.x, b = blockIdx.x;
-    if ((nblk & 7u) == 0u) b = (b & 7u) * (nblk >> 3) + (b >> 3);
-    const int ncx = g.cps_x >> 1, ncy = g.cps_y >> 1, ncz = g.nz_local >> 1;
-    const int total = ncx * ncy * ncz;
-    const int t = (int)b * kSubWaves + wv;
-    if (t >= total) return;
+    const int ncx = g.cps_x >> 1, ncy = g.cps_y >> 1;
     const int ta = wave_uniform(t % ncx);
     const int tb = wave_uniform((t / ncx) % ncy);
     const int tc = wave_uniform(t / (ncx * ncy));
@@ -176,7 +168,8 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep(DevGeom g, float
     rng_chunk(0, true);
 
     const int n_own = __builtin_amdgcn_readfirstlane(k_cnt);   // lane 0 = own cell
-    if (n_own == 0) return;                                     // subsweep.h:252-253
+    if (n_own == 0) return true;                                // subsweep.h:252-253
+    const int cap_nb = cap - n_own;
     if (n_own > 32) {     // nmax > 32: Fisher-Yates words of slots 32..63
         const pmc_u32x4 w = pmc_philox4x32_10((uint32_t)lane, id, sweep, PMC_TAG_SHUFFLE, k0, k1);
         if (lane >= 32) jv = (int)pmc_bounded(w.v[0], (uint32_t)(lane + 1));
@@ -206,15 +199,16 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep(DevGeom g, float
         const float uz = vz[q] + __shfl(k_sz, ks);
         const bool keep = (k < 27) && (p < cnt) && (pmc_box_d2(ux, uy, uz, blo, bhi) <= g.rc2f);
         const unsigned long long mk = __ballot(keep);
-        if (keep) {
-            const int dst = S_nb + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
-                                               __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+        const int dst = S_nb + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
+                                           __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+        if (keep && dst < cap_nb) {
             px_[dst] = ux;
             py_[dst] = uy;
             pz_[dst] = uz;
         }
         S_nb += __popcll(mk);
     }
+    if (S_nb > cap_nb) return false;                            // -> full-capacity fallback
     {
         const float sxo = as_f(__shfl(as_i(ownx), perm));
         const float syo = as_f(__shfl(as_i(owny), perm));
@@ -267,15 +261,15 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep(DevGeom g, float
                     for (; k0p + kWave <= S_nb; k0p += kWave) {
                         const int k = k0p + lane;
                         const float xj = px_[k], yj = py_[k], zj = pz_[k];
-                        newp = newp + pmc_lj_from_r2(pmc_r2(qx - xj, qy - yj, qz - zj), rc2);
+                        newp = newp + pmc_lj4_from_r2(pmc_r2(qx - xj, qy - yj, qz - zj), rc2);
                     }
                 }
                 for (; k0p < K; k0p += kWave) {
                     const int k = k0p + lane;
                     const int kr = k < K ? k : 0;
                     const float xj = px_[kr], yj = py_[kr], zj = pz_[kr];
-                    const float en = pmc_lj_from_r2(pmc_r2(qx - xj, qy - yj, qz - zj), rc2);
-                    const float eo = pmc_lj_from_r2(pmc_r2(xi - xj, yi - yj, zi - zj), rc2);
+                    const float en = pmc_lj4_from_r2(pmc_r2(qx - xj, qy - yj, qz - zj), rc2);
+                    const float eo = pmc_lj4_from_r2(pmc_r2(xi - xj, yi - yj, zi - zj), rc2);
                     const bool is_nb = k < S_nb;
                     const bool is_own = (k >= S_nb) && (k < K) && (k - S_nb != i);
                     newp = newp + (is_nb ? en : 0.0f);
@@ -283,7 +277,9 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep(DevGeom g, float
                     down = down + (is_own ? (en - eo) : 0.0f);
                 }
                 if (cached) oldp = cache[i * kWave + lane];
-                const float v = down + (newp - oldp);
+                // quarter energies were accumulated; the factor 4 is exact, so 4*(sum of u)
+                // equals the sum of the 4u the oracle accumulates, bit for bit
+                const float v = 4.0f * (down + (newp - oldp));
                 const float dE = wave_sum_fixed_order(v);
                 const bool accept = beta_d * (double)dE < (double)Tm;   // accept_move, subsweep.h:209-216
                 // keep the partials only if slot i moves again in this visit and fits the cache
@@ -315,6 +311,49 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep(DevGeom g, float
         atomicAdd(&stats[1 * kStatSlots + slot], (unsigned long long)n_acc);
         atomicAdd(&stats[2 * kStatSlots + slot], (unsigned long long)g.n_moves);
         atomicAdd(&stats[3 * kStatSlots + slot], (unsigned long long)n_ev);
+    }
+    return true;
+}
+
+// Main launch: one wave per cell of the colour; LDS capacity `cap` partners per wave (sized for
+// the occupancy; a cell whose filtered stencil exceeds it is queued in ovf for the fallback).
+template <int NSLOT, int NMC>
+__global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep(DevGeom g, float* __restrict__ disk,
+                                                                  const int16_t* __restrict__ ncnt,
+                                                                  int ox, int oy, int oz, uint32_t sweep,
+                                                                  unsigned long long* __restrict__ stats,
+                                                                  int cap, int* __restrict__ ovf) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int wv = threadIdx.x >> 6;
+    float* px_ = smem + wv * (3 * cap + kWave * g.ncache);
+    // XCD-aware block order: blocks b and b+8 share an XCD (round-robin dispatch), so give each
+    // XCD a contiguous run of cells -> neighbouring stencils share that XCD's L2.  Speed only.
+    uint32_t nblk = gridDim.x, b = blockIdx.x;
+    if ((nblk & 7u) == 0u) b = (b & 7u) * (nblk >> 3) + (b >> 3);
+    const int total = (g.cps_x >> 1) * (g.cps_y >> 1) * (g.nz_local >> 1);
+    const int t = (int)b * kSubWaves + wv;
+    if (t >= total) return;
+    if (!subsweep_wave<NSLOT, NMC>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, cap, t)) {
+        if ((threadIdx.x & (kWave - 1)) == 0) ovf[1 + atomicAdd(&ovf[0], 1)] = t;
+    }
+}
+
+// Fallback launch: full capacity (27*nmax partners per wave), a fixed grid striding over the
+// queued cells.  Cells of one colour are independent, so the order does not matter.
+template <int NSLOT, int NMC>
+__global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_fallback(DevGeom g, float* __restrict__ disk,
+                                                                           const int16_t* __restrict__ ncnt,
+                                                                           int ox, int oy, int oz, uint32_t sweep,
+                                                                           unsigned long long* __restrict__ stats,
+                                                                           int* __restrict__ ovf) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int wv = threadIdx.x >> 6;
+    const int cap = 27 * (NMC > 0 ? NMC : g.nmax);
+    float* px_ = smem + wv * (3 * cap + kWave * g.ncache);
+    const int count = __builtin_amdgcn_readfirstlane(ovf[0]);
+    for (int e = (int)blockIdx.x * kSubWaves + wv; e < count; e += (int)gridDim.x * kSubWaves) {
+        const int t = __builtin_amdgcn_readfirstlane(ovf[1 + e]);
+        (void)subsweep_wave<NSLOT, NMC>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, cap, t);
     }
 }
 
@@ -554,24 +593,49 @@ __global__ void k_selftest(const uint32_t* __restrict__ words, int count, float*
 // ------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------
-hipError_t launch_subsweep(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
-                           uint32_t sweep, unsigned long long* stats, hipStream_t st) {
+int subsweep_capacity(const DevGeom& g) {
+    // Partners per wave held in LDS by the main launch.  Sized so a wave needs at most 5 KiB of
+    // LDS (-> 32 waves/CU, the hardware limit): 3 floats per partner + 64 floats per cache slot.
+    // The filtered stencil holds ~98 partners at n = 4.77 per cell; larger ones use the fallback.
+    const int full = 27 * g.nmax;
+    // test hook: PMC_SUBSWEEP_CAP forces a (small) capacity so the fallback path is exercised
+    static const int forced = [] {
+        const char* e = std::getenv("PMC_SUBSWEEP_CAP");
+        return e ? std::atoi(e) : 0;
+    }();
+    if (forced > 0) return forced < full ? forced : full;
+    const int cap = (5120 / 4 - kWave * g.ncache) / 3;
+    if (cap < 128) return full;
+    return cap < full ? cap : full;
+}
+
+template <int NSLOT, int NMC>
+static void launch_subsweep_t(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
+                              uint32_t sweep, unsigned long long* stats, int* ovf, hipStream_t st) {
     const int64_t total = (int64_t)(g.cps_x / 2) * (g.cps_y / 2) * (g.nz_local / 2);
     const int64_t blocks = (total + kSubWaves - 1) / kSubWaves;
-    const size_t lds = sizeof(float) * (3 * 27 * (size_t)g.nmax + kWave * (size_t)g.ncache) * kSubWaves;
-    dim3 grid((unsigned)blocks), block(kWave * kSubWaves);
-    if (g.nmax == 16) {
-        hipLaunchKernelGGL((k_subsweep<16, 16>), grid, block, lds, st, g, disk, n, ox, oy, oz, sweep, stats);
-    } else if (g.nmax == 32) {
-        hipLaunchKernelGGL((k_subsweep<32, 32>), grid, block, lds, st, g, disk, n, ox, oy, oz, sweep, stats);
-    } else {
-        switch (g.nslot) {
-            case 8: hipLaunchKernelGGL((k_subsweep<8, 0>), grid, block, lds, st, g, disk, n, ox, oy, oz, sweep, stats); break;
-            case 16: hipLaunchKernelGGL((k_subsweep<16, 0>), grid, block, lds, st, g, disk, n, ox, oy, oz, sweep, stats); break;
-            case 32: hipLaunchKernelGGL((k_subsweep<32, 0>), grid, block, lds, st, g, disk, n, ox, oy, oz, sweep, stats); break;
-            default: hipLaunchKernelGGL((k_subsweep<64, 0>), grid, block, lds, st, g, disk, n, ox, oy, oz, sweep, stats); break;
-        }
+    const int cap = subsweep_capacity(g);
+    const int full = 27 * g.nmax;
+    const size_t lds = sizeof(float) * (3 * (size_t)cap + kWave * (size_t)g.ncache) * kSubWaves;
+    hipLaunchKernelGGL((k_subsweep<NSLOT, NMC>), dim3((unsigned)blocks), dim3(kWave * kSubWaves), lds, st, g,
+                       disk, n, ox, oy, oz, sweep, stats, cap, ovf);
+    if (cap < full) {
+        const size_t lds_full = sizeof(float) * (3 * (size_t)full + kWave * (size_t)g.ncache) * kSubWaves;
+        hipLaunchKernelGGL((k_subsweep_fallback<NSLOT, NMC>), dim3(64), dim3(kWave * kSubWaves), lds_full, st,
+                           g, disk, n, ox, oy, oz, sweep, stats, ovf);
     }
+}
+
+hipError_t launch_subsweep(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
+                           uint32_t sweep, unsigned long long* stats, int* ovf, hipStream_t st) {
+    hipError_t e = hipMemsetAsync(ovf, 0, sizeof(int), st);
+    if (e != hipSuccess) return e;
+    if (g.nmax == 16) launch_subsweep_t<16, 16>(g, disk, n, ox, oy, oz, sweep, stats, ovf, st);
+    else if (g.nmax == 32) launch_subsweep_t<32, 32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, st);
+    else if (g.nslot == 8) launch_subsweep_t<8, 0>(g, disk, n, ox, oy, oz, sweep, stats, ovf, st);
+    else if (g.nslot == 16) launch_subsweep_t<16, 0>(g, disk, n, ox, oy, oz, sweep, stats, ovf, st);
+    else if (g.nslot == 32) launch_subsweep_t<32, 0>(g, disk, n, ox, oy, oz, sweep, stats, ovf, st);
+    else launch_subsweep_t<64, 0>(g, disk, n, ox, oy, oz, sweep, stats, ovf, st);
     return hipGetLastError();
 }
 

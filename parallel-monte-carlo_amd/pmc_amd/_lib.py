@@ -11,7 +11,7 @@ import subprocess
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))   # parallel-monte-carlo_amd/
 REPO_DIR = os.path.dirname(PKG_DIR)
-LIB_PATH = os.path.join(PKG_DIR, "build", "libpmc.so")
+LIB_PATH = os.environ.get("PMC_LIB_PATH") or os.path.join(PKG_DIR, "build", "libpmc.so")
 START_PATH = os.path.join(PKG_DIR, "build", "start")
 HEADER = os.path.join(REPO_DIR, "include", "pmc.h")
 
