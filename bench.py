@@ -89,6 +89,7 @@ def main() -> int:
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--graph", action="store_true", help="replay the timed sweeps as one hipGraph")
+    ap.add_argument("--slab", action="store_true", help="use the z-slab/halo path even with one rank")
     args = ap.parse_args()
 
     import torch
@@ -111,7 +112,8 @@ def main() -> int:
         if world > 1:
             dist.barrier()
 
-    if world == 1:
+    slab = world > 1 or args.slab
+    if not slab:
         sim = pmc_amd.PmcContext(cps, stream=stream.cuda_stream)
         sim.init_lattice(args.atoms)
         run_phase = sim.phase
@@ -164,9 +166,9 @@ def main() -> int:
     # algorithmic bytes from the state at the start of the timed region
     disk_h, n_h = sim.copy_out()
     plane = cps * cps
-    lo = plane if world > 1 else 0
+    lo = plane if slab else 0
     n_owned = n_h[lo:lo + plane * cps].astype(np.int64)
-    if world == 1:
+    if not slab:
         stencil = stencil_counts(n_owned, (cps, cps, cps))
     else:
         ext = n_h.astype(np.int64).reshape(cps + 2, cps, cps)
@@ -184,7 +186,7 @@ def main() -> int:
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     first = args.warmup
-    if args.graph and world == 1:
+    if args.graph and not slab:
         sim.run_graph(first, args.steps)
     else:
         for k in range(args.steps):
@@ -218,7 +220,7 @@ def main() -> int:
                 "launch_ms": avg_launch_s * 1e3 if avg_launch_s else None,
                 "algorithmic_bytes_per_launch": abytes["subsweep_launch"]}
         cpu = None
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline and not slab:
             try:
                 thr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
                 cpu = cpu_baseline(disk_h, n_h, cps, args.cpu_sweeps, thr, first)
@@ -242,7 +244,7 @@ def main() -> int:
                                    f"sweep (8 colour phases + shiftCells), box {cps}x{cps}x{cps_z}",
                        "cells_per_gpu": cps ** 3, "particles_per_gpu": args.atoms, "n_moves": 10,
                        "nmax": 16, "beta": 0.3, "sigma": 0.5, "w": 2.5,
-                       "parallelism": f"z-slab x{world}" if world > 1 else "single GPU"},
+                       "parallelism": f"z-slab x{world} (RCCL halo planes)" if slab else "single GPU"},
             "sweeps_per_s": sweeps_per_s,
             "acceptance": st["accepted"] / st["trials"] if st["trials"] else None,
             "error_flags": flags,

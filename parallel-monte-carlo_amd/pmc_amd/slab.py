@@ -1,0 +1,207 @@
+"""z-slab domain decomposition over ranks (one process per GPU), halo planes over RCCL.
+
+The reference is single-GPU (start.cu:169-272); this is the build's multi-GPU path (SURVEY.md
+section 8e).  Rank r owns global cell planes z in [r*nz, (r+1)*nz) of a cps x cps x (world*nz)
+periodic box and stores one halo plane below and above (pmc_params.halo = 1).  Every rank runs
+every colour phase on its slab; the checkerboard guarantees that a phase only READS the halo
+planes, and only the boundary plane of the phase's z-parity changes:
+
+  * after a phase with oz = 0 the owned plane 0 changed  -> it becomes the top halo of rank r-1;
+  * after a phase with oz = 1 the owned plane nz-1 changed -> the bottom halo of rank r+1;
+  * after shiftCells every plane (and the counts) may change -> both halos are refreshed.
+
+The sweep plan (colour order, f, d) is a pure function of (seed, sweep) that every rank derives
+itself, and the RNG counters use GLOBAL cell ids, so the result is bit-identical to the
+whole-box run for any number of ranks (tests/test_slab.py checks 2 ranks against 1).
+
+The engine and the transport are injected: the product path uses PmcContext (HIP) with torch
+device tensors and torch.distributed point-to-point (backend "nccl" = RCCL over xGMI); the CPU
+tests drive the same class with the C oracle and the gloo backend.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, List, Optional, Tuple
+
+from .plan import sweep_plan
+
+
+@dataclass
+class SlabGeometry:
+    cps: int          # cells along x and y
+    nz: int           # owned planes per rank (even)
+    rank: int
+    world: int
+    nmax: int
+
+    @property
+    def cps_z(self) -> int:
+        return self.nz * self.world
+
+    @property
+    def z0(self) -> int:
+        return self.rank * self.nz
+
+    @property
+    def below(self) -> int:
+        return (self.rank - 1) % self.world
+
+    @property
+    def above(self) -> int:
+        return (self.rank + 1) % self.world
+
+
+class TorchP2P:
+    """Halo transport over torch.distributed point-to-point (nccl/RCCL or gloo)."""
+
+    def __init__(self, rank: int, world: int, group=None):
+        self.rank = rank
+        self.world = world
+        self.group = group
+
+    def exchange(self, sends: List[Tuple[object, int]], recvs: List[Tuple[object, int]]) -> None:
+        """sends/recvs: (tensor, peer).  Every rank issues its sends and receives in the same
+        logical order (down-plane first, then up-plane), which fixes the pairwise matching."""
+        import torch.distributed as dist
+        if self.world == 1:
+            # periodic single-rank slab: each receive takes the send with the same role
+            for (dst, _), (src, _) in zip(recvs, sends_for_self(sends, recvs)):
+                dst.copy_(src)
+            return
+        ops = [dist.P2POp(dist.isend, t, p, group=self.group) for t, p in sends]
+        ops += [dist.P2POp(dist.irecv, t, p, group=self.group) for t, p in recvs]
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+
+
+def sends_for_self(sends, recvs):
+    """world == 1: the i-th receive is filled from the matching send (same order contract)."""
+    return sends[: len(recvs)]
+
+
+class SlabSimulation:
+    """Checkerboard sweeps on one z-slab with halo exchange after every phase and shift.
+
+    engine: object with phase(colour, sweep) and shift(sweep) acting on buffer `cur`, flipping
+            `cur` in shift (PmcContext with attached state, or the test's oracle engine).
+    disk/n: the two state buffers [buf0, buf1] as tensors of shape (nz+2, cps, cps, 3, nmax)
+            and (nz+2, cps, cps) (storage plane 0 is the bottom halo, plane nz+1 the top halo).
+    """
+
+    def __init__(self, engine, geom: SlabGeometry, disk: list, n: list, transport, seed: int = 1234,
+                 w: float = 2.5, plan_fn: Optional[Callable] = None):
+        self.engine = engine
+        self.g = geom
+        self.disk = disk
+        self.n = n
+        self.tp = transport
+        self.seed = seed
+        self.w = w
+        self.cur = 0
+        self.plan_fn = plan_fn or sweep_plan
+
+    # ---- construction of the product path -------------------------------------------------
+    @classmethod
+    def create(cls, cps: int, nz_local: int, rank: int, world: int, stream=None, atoms_per_rank: int = 0,
+               nmax: int = 16, n_moves: int = 10, seed: int = 1234, group=None, **kw):
+        """HIP engine on the current device; state in torch device tensors; RCCL transport."""
+        import torch
+        from .engine import PmcContext
+        g = SlabGeometry(cps, nz_local, rank, world, nmax)
+        if stream is None:                 # kernels and halo copies must share ONE stream
+            stream = torch.cuda.Stream()
+        ctx = PmcContext(cps, cps_z=g.cps_z, nz_local=nz_local, z0=g.z0, halo=1, nmax=nmax, n_moves=n_moves,
+                         seed=seed, stream=stream.cuda_stream, **kw)
+        dev = torch.device("cuda", torch.cuda.current_device())
+        shape = (nz_local + 2, cps, cps, 3, nmax)
+        disk = [torch.zeros(shape, dtype=torch.float32, device=dev) for _ in range(2)]
+        n = [torch.zeros(shape[:3], dtype=torch.int16, device=dev) for _ in range(2)]
+        torch.cuda.synchronize()
+        ctx.attach_state(disk[0], n[0], disk[1], n[1])
+        sim = cls(ctx, g, disk, n, TorchP2P(rank, world, group), seed=seed)
+        sim.stream = stream
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier(group=group)      # a collective first, then point-to-point (NCCL rule)
+        if atoms_per_rank:
+            ctx.init_lattice(atoms_per_rank)
+            sim.exchange_full()
+        return sim
+
+    @property
+    def ctx(self):
+        return self.engine
+
+    # ---- halo exchange ------------------------------------------------------------------
+    def _plane(self, z_local: int, with_n: bool):
+        import torch
+        d = self.disk[self.cur][z_local + 1]
+        if not with_n:
+            return d, None
+        # counts travel as bytes: NCCL/RCCL has no 16-bit integer type
+        return d, self.n[self.cur][z_local + 1].view(torch.uint8)
+
+    def _exchange(self, send_down: bool, send_up: bool, with_n: bool) -> None:
+        g = self.g
+        sends, recvs = [], []
+        if send_down:   # my plane 0 -> top halo of the rank below; my top halo <- plane 0 of above
+            d, nn = self._plane(0, with_n)
+            sends.append((d, g.below))
+            rd, rn = self._plane(g.nz, with_n)
+            recvs.append((rd, g.above))
+            if with_n:
+                sends.append((nn, g.below))
+                recvs.append((rn, g.above))
+        if send_up:     # my plane nz-1 -> bottom halo of the rank above; my bottom halo <- below
+            d, nn = self._plane(g.nz - 1, with_n)
+            sends.append((d, g.above))
+            rd, rn = self._plane(-1, with_n)
+            recvs.append((rd, g.below))
+            if with_n:
+                sends.append((nn, g.above))
+                recvs.append((rn, g.below))
+        self._run(sends, recvs)
+
+    def _run(self, sends, recvs):
+        stream = getattr(self, "stream", None)
+        if stream is not None:
+            import torch
+            with torch.cuda.stream(stream):
+                self.tp.exchange(sends, recvs)
+        else:
+            self.tp.exchange(sends, recvs)
+
+    def exchange_after_phase(self, colour: int) -> None:
+        oz = colour % 2          # itoa (start.cu:153-157): offset[2] = colour % 2
+        self._exchange(send_down=(oz == 0), send_up=(oz == 1), with_n=False)
+
+    def exchange_after_shift(self) -> None:
+        self._exchange(True, True, with_n=True)
+
+    def exchange_full(self) -> None:
+        self.exchange_after_shift()
+
+    # ---- driver (start.cu:237-260 per slab) -------------------------------------------------
+    def phase_only(self, colour: int, sweep: int) -> None:
+        self.engine.phase(colour, sweep)
+
+    def shift_only(self, sweep: int) -> None:
+        self.engine.shift(sweep)
+        self.cur ^= 1
+
+    def sweep(self, s: int) -> None:
+        order, _, _ = self.plan_fn(self.seed, s, self.w)
+        for colour in order:
+            self.phase_only(colour, s)
+            self.exchange_after_phase(colour)
+        self.shift_only(s)
+        self.exchange_after_shift()
+
+    def run(self, first: int, count: int) -> None:
+        for k in range(count):
+            self.sweep(first + k)
+
+    # ---- views ------------------------------------------------------------------------
+    def owned(self):
+        """(disk, n) of the owned planes of the current buffer."""
+        return self.disk[self.cur][1:-1], self.n[self.cur][1:-1]

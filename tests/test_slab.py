@@ -1,0 +1,61 @@
+"""Slab decomposition (multi-GPU path) on CPU: 2 gloo ranks driving the oracle through the same
+SlabSimulation class the RCCL product path uses; the result must equal the whole-box run
+bit for bit (global-id RNG counters, replicated sweep plan, halo exchange schedule)."""
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+import slab_helpers
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world,nz", [(2, 4), (2, 8), (3, 4)])
+def test_slab_ranks_equal_whole_box(oracle, world, nz):
+    cps, nmax, atoms, sweeps = 8, 16, 1000, 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=slab_helpers.worker, args=(r, world, port, cps, nz, nmax, atoms, sweeps, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        rank, init, final, stats = q.get(timeout=300)
+        res[rank] = (init, final, stats)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # whole box, same initial state, same sweeps
+    st = slab_helpers.whole_box_from_slabs(cps, nz, world, nmax, [res[r][0][0] for r in range(world)],
+                                           [res[r][0][1] for r in range(world)])
+    assert int(st.n.sum()) == atoms * world
+    assert st.run(0, sweeps) == 0
+    got_d = np.concatenate([res[r][1][0].reshape(-1) for r in range(world)])
+    got_n = np.concatenate([res[r][1][1].reshape(-1) for r in range(world)])
+    assert np.array_equal(got_n, st.n)
+    assert oracle.valid_slots_equal(got_d, got_n, st.disk, st.n, nmax)
+    tot = {k: sum(res[r][2][k] for r in range(world)) for k in res[0][2]}
+    assert tot == st.stats.as_dict()
+
+
+def test_slab_single_rank_periodic(oracle):
+    """world == 1 slab (halo planes filled by local copies) equals the whole box."""
+    from pmc_amd.slab import TorchP2P
+    sim = slab_helpers.make_oracle_slab(8, 8, 0, 1, 16, 1500, TorchP2P(0, 1))
+    d0, n0 = sim.owned()
+    st = slab_helpers.whole_box_from_slabs(8, 8, 1, 16, [d0.numpy().copy()], [n0.numpy().copy()])
+    sim.run(0, 3)
+    st.run(0, 3)
+    d1, n1 = sim.owned()
+    assert np.array_equal(n1.numpy().reshape(-1), st.n)
+    assert oracle.valid_slots_equal(d1.numpy().reshape(-1), n1.numpy().reshape(-1), st.disk, st.n, 16)
