@@ -249,21 +249,30 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
             const float qy = yi + g1 * g.sigma;
             const float qz = zi + g2 * g.sigma;
             const float ddx = qx - cxf, ddy = qy - cyf, ddz = qz - czf;
-            const bool out = (ddx > hw) || (ddx < -hw) || (ddy > hw) || (ddy < -hw) || (ddz > hw) ||
-                             (ddz < -hw);
+            // (d > hw || d < -hw) == (|d| > hw) for non-NaN d; |d| is a free source modifier
+            const bool out = (__builtin_fabsf(ddx) > hw) || (__builtin_fabsf(ddy) > hw) ||
+                             (__builtin_fabsf(ddz) > hw);
             if (!out) {
                 ++n_ev;
                 const bool cached = (cvalid >> i) & 1ull;
                 float newp = 0.0f, oldp = 0.0f, down = 0.0f;
                 int k0p = 0;
-                if (cached) {
-                    // neighbour-only passes: new energies only
+                // passes entirely inside the neighbour list: no own-cell bookkeeping
+                if (cached) {   // new energies only (old partials come from the cache)
                     for (; k0p + kWave <= S_nb; k0p += kWave) {
                         const int k = k0p + lane;
                         const float xj = px_[k], yj = py_[k], zj = pz_[k];
                         newp = newp + pmc_lj4_from_r2(pmc_r2(qx - xj, qy - yj, qz - zj), rc2);
                     }
+                } else {
+                    for (; k0p + kWave <= S_nb; k0p += kWave) {
+                        const int k = k0p + lane;
+                        const float xj = px_[k], yj = py_[k], zj = pz_[k];
+                        newp = newp + pmc_lj4_from_r2(pmc_r2(qx - xj, qy - yj, qz - zj), rc2);
+                        oldp = oldp + pmc_lj4_from_r2(pmc_r2(xi - xj, yi - yj, zi - zj), rc2);
+                    }
                 }
+                // tail pass(es): the rest of the neighbours + the own cell
                 for (; k0p < K; k0p += kWave) {
                     const int k = k0p + lane;
                     const int kr = k < K ? k : 0;
@@ -324,7 +333,7 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep(DevGeom g, float
                                                                   unsigned long long* __restrict__ stats,
                                                                   int cap, int* __restrict__ ovf) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int wv = threadIdx.x >> 6;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform -> SALU math
     float* px_ = smem + wv * (3 * cap + kWave * g.ncache);
     // XCD-aware block order: blocks b and b+8 share an XCD (round-robin dispatch), so give each
     // XCD a contiguous run of cells -> neighbouring stencils share that XCD's L2.  Speed only.
@@ -347,7 +356,7 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_fallback(DevGeom
                                                                            unsigned long long* __restrict__ stats,
                                                                            int* __restrict__ ovf) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int wv = threadIdx.x >> 6;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int cap = 27 * (NMC > 0 ? NMC : g.nmax);
     float* px_ = smem + wv * (3 * cap + kWave * g.ncache);
     const int count = __builtin_amdgcn_readfirstlane(ovf[0]);
