@@ -113,54 +113,50 @@ def main() -> int:
             dist.barrier()
 
     slab = world > 1 or args.slab
+    events = []      # (kind, start, end) HIP events on the kernels' stream
+
+    def timer(kind, fn, record):
+        if not record:
+            return fn()
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        fn()
+        b.record(stream)
+        events.append((kind, a, b))
+
     if not slab:
         sim = pmc_amd.PmcContext(cps, stream=stream.cuda_stream)
         sim.init_lattice(args.atoms)
-        run_phase = sim.phase
-        run_shift = sim.shift
-        halo_after_phase = lambda colour: None  # noqa: E731
-        halo_after_shift = lambda: None  # noqa: E731
+        from pmc_amd.plan import sweep_plan
+        plans = {}
+
+        def one_sweep(s, record):
+            if s not in plans:
+                plans[s] = sweep_plan(1234, s, 2.5)
+            for colour in plans[s][0]:
+                timer("phase", lambda: sim.phase(colour, s), record)
+            timer("shift", lambda: sim.shift(s), record)
+
+        def finish():
+            pass
         cps_z = cps
     else:
         from pmc_amd.slab import SlabSimulation
         sim_s = SlabSimulation.create(cps=cps, nz_local=cps, rank=rank, world=world, stream=stream,
                                       atoms_per_rank=args.atoms)
         sim = sim_s.ctx
-        run_phase = sim_s.phase_only
-        run_shift = sim_s.shift_only
-        halo_after_phase = sim_s.exchange_after_phase
-        halo_after_shift = sim_s.exchange_after_shift
+
+        def one_sweep(s, record):
+            sim_s.sweep(s, timer=lambda kind, fn: timer(kind, fn, record))
+
+        finish = sim_s.finish
         cps_z = cps * world
-
-    plan_cache = {}
-
-    def plan(s):
-        if s not in plan_cache:
-            sys.path.insert(0, os.path.join(REPO, "parallel-monte-carlo_amd"))
-            from pmc_amd.plan import sweep_plan
-            plan_cache[s] = sweep_plan(1234, s, 2.5)
-        return plan_cache[s]
-
-    events = []
-
-    def one_sweep(s, record):
-        order, _, _ = plan(s)
-        for colour in order:
-            if record:
-                a = torch.cuda.Event(enable_timing=True)
-                b = torch.cuda.Event(enable_timing=True)
-                a.record(stream)
-            run_phase(colour, s)
-            if record:
-                b.record(stream)
-                events.append((a, b))
-            halo_after_phase(colour)
-        run_shift(s)
-        halo_after_shift()
 
     # warmup
     for s in range(args.warmup):
         one_sweep(s, False)
+    finish()
     torch.cuda.synchronize()
     sim.stats(reset=True)
     # algorithmic bytes from the state at the start of the timed region
@@ -191,12 +187,17 @@ def main() -> int:
     else:
         for k in range(args.steps):
             one_sweep(first + k, True)
+        finish()
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
     st = sim.stats()
     trials_local = st["trials"]
-    phase_ms = [a.elapsed_time(b) for a, b in events] if events else []
+    # kernel time of one colour phase = sum of its launches (the slab path splits a phase into the
+    # interior and the two boundary planes); 8 phases per sweep
+    phase_total_ms = sum(a.elapsed_time(b) for kind, a, b in events if kind == "phase")
+    shift_total_ms = sum(a.elapsed_time(b) for kind, a, b in events if kind == "shift")
+    n_phases = 8 * args.steps if events else 0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -210,7 +211,7 @@ def main() -> int:
     value = trials_total / elapsed
 
     if rank == 0:
-        avg_launch_s = (float(np.mean(phase_ms)) * 1e-3) if phase_ms else None
+        avg_launch_s = (phase_total_ms / n_phases * 1e-3) if n_phases else None
         achieved = (abytes["subsweep_launch"] / avg_launch_s / 1e9) if avg_launch_s else None
         traffic = traffic_from_profile()
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -218,6 +219,7 @@ def main() -> int:
                 "traffic": traffic.get("subsweep_bytes_per_launch") if traffic else None,
                 "kernel": "k_subsweep<16> (one colour phase)",
                 "launch_ms": avg_launch_s * 1e3 if avg_launch_s else None,
+                "shift_ms": shift_total_ms / args.steps if n_phases else None,
                 "algorithmic_bytes_per_launch": abytes["subsweep_launch"]}
         cpu = None
         if not args.no_cpu_baseline and not slab:

@@ -122,6 +122,12 @@ int pmc_sweep(pmc_ctx* ctx, uint32_t sweep);
  * context state (any mode; the slab driver interleaves these with halo exchange). */
 int pmc_phase(pmc_ctx* ctx, int colour, uint32_t sweep);
 int pmc_shift(pmc_ctx* ctx, uint32_t sweep);
+/* Restrict a colour phase to the cells in local planes [zl_begin, zl_end) (0 <= .. <= nz_local).
+ * Cells of one colour are independent, so splitting a phase into ranges in any order gives the
+ * same result; the slab driver runs the halo-free interior while boundary planes travel. */
+int pmc_subsweep_range(pmc_ctx* ctx, float* d_disk, const int16_t* d_n, const int offset[3],
+                       uint32_t sweep, int zl_begin, int zl_end);
+int pmc_phase_range(pmc_ctx* ctx, int colour, uint32_t sweep, int zl_begin, int zl_end);
 /* The per-sweep plan every rank replicates (no broadcast): colour order (FY_Shuffle + itoa,
  * start.cu:34-44,153-157, reseeded from time() in the reference) and the shift axis/distance
  * (kernel.cu:683-684), all from the host Philox stream keyed by `seed`. */

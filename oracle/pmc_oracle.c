@@ -287,8 +287,19 @@ static void subsweep_cell(const pmc_params* p, float* disk, const int16_t* n, in
 
 void orc_subsweep(const pmc_params* p, float* disk, const int16_t* n, int ox, int oy, int oz,
                   uint32_t sweep, pmc_stats* st) {
+    orc_subsweep_range(p, disk, n, ox, oy, oz, sweep, 0, p->nz_local, st);
+}
+
+/* the cells of the colour in local planes [zl_begin, zl_end) */
+void orc_subsweep_range(const pmc_params* p, float* disk, const int16_t* n, int ox, int oy, int oz,
+                        uint32_t sweep, int zl_begin, int zl_end, pmc_stats* st) {
     const float rc2 = pmc_cutoff_r2(p->w);
-    const int ncx = p->cps_x / 2, ncy = p->cps_y / 2, ncz = p->nz_local / 2;
+    const int ncx = p->cps_x / 2, ncy = p->cps_y / 2;
+    int cz0 = zl_begin - oz <= 0 ? 0 : (zl_begin - oz + 1) / 2;
+    int cz1 = zl_end - oz <= 0 ? 0 : (zl_end - oz + 1) / 2;
+    if (cz1 > p->nz_local / 2) cz1 = p->nz_local / 2;
+    if (cz1 <= cz0) return;
+    const int ncz = cz1 - cz0;
     const int64_t total = (int64_t)ncx * ncy * ncz;
     const int cap = 27 * p->nmax;
     int64_t de = 0, acc = 0, tri = 0, ev = 0;
@@ -304,7 +315,7 @@ void orc_subsweep(const pmc_params* p, float* disk, const int16_t* n, int ox, in
 #endif
         for (int64_t t = 0; t < total; ++t) {
             int a = (int)(t % ncx), b = (int)((t / ncx) % ncy), cz = (int)(t / ((int64_t)ncx * ncy));
-            subsweep_cell(p, disk, n, 2 * a + ox, 2 * b + oy, 2 * cz + oz, sweep, rc2, xs, ys, zs,
+            subsweep_cell(p, disk, n, 2 * a + ox, 2 * b + oy, 2 * (cz0 + cz) + oz, sweep, rc2, xs, ys, zs,
                           &de, &acc, &tri, &ev);
         }
         free(buf);

@@ -37,6 +37,8 @@ int orc_assign(const pmc_params* p, const float* r, int64_t n_atoms, float* disk
 /* subsweep_kernel (subsweep.h:240-300) -- one colour phase */
 void orc_subsweep(const pmc_params* p, float* disk, const int16_t* n, int ox, int oy, int oz,
                   uint32_t sweep, pmc_stats* st);
+void orc_subsweep_range(const pmc_params* p, float* disk, const int16_t* n, int ox, int oy, int oz,
+                        uint32_t sweep, int zl_begin, int zl_end, pmc_stats* st);
 /* shiftCells (CUDA-Parallel-MC/CUDA-Parallel-MC/shiftCells.h:23-112) -- returns overflow count */
 int orc_shift_cells(const pmc_params* p, const float* din, const int16_t* nin, float* dout,
                     int16_t* nout, int f, float d);

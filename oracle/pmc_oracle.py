@@ -72,6 +72,9 @@ def lib():
         L.orc_subsweep.argtypes = [P, _f32p, _i16p, C.c_int, C.c_int, C.c_int, C.c_uint32,
                                    C.POINTER(Stats)]
         L.orc_subsweep.restype = None
+        L.orc_subsweep_range.argtypes = [P, _f32p, _i16p, C.c_int, C.c_int, C.c_int, C.c_uint32, C.c_int,
+                                         C.c_int, C.POINTER(Stats)]
+        L.orc_subsweep_range.restype = None
         L.orc_shift_cells.argtypes = [P, _f32p, _i16p, _f32p, _i16p, C.c_int, C.c_float]
         L.orc_energy.argtypes = [P, _f32p, _i16p]
         L.orc_energy.restype = C.c_double

@@ -137,7 +137,7 @@ int enqueue_sweep(pmc_ctx* c, uint32_t sweep) {
         int o[3];
         pmc_colour_offset(plan.order[k], o);
         hipError_t e = launch_subsweep(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep,
-                                       c->stats, c->ovf, c->stream);
+                                       c->stats, c->ovf, 0, c->P.nz_local, c->stream);
         if (e != hipSuccess) return hip_fail(e, "subsweep launch");
     }
     hipError_t e = launch_shift(c->G, c->disk[c->cur], c->n[c->cur], c->disk[c->cur ^ 1], c->n[c->cur ^ 1],
@@ -266,13 +266,21 @@ int pmc_assign(pmc_ctx* c, const float* d_r, int64_t n_atoms, float* d_disk, int
     return PMC_OK;
 }
 
-int pmc_subsweep(pmc_ctx* c, float* d_disk, const int16_t* d_n, const int offset[3], uint32_t sweep) {
+int pmc_subsweep_range(pmc_ctx* c, float* d_disk, const int16_t* d_n, const int offset[3], uint32_t sweep,
+                       int zl_begin, int zl_end) {
     if (!c || !d_disk || !d_n || !offset) return fail(PMC_ERR_ARG, "bad argument");
     for (int k = 0; k < 3; ++k)
         if (offset[k] != 0 && offset[k] != 1) return fail(PMC_ERR_ARG, "offset must be in {0,1}^3");
+    if (zl_begin < 0 || zl_end > c->P.nz_local || zl_begin > zl_end)
+        return fail(PMC_ERR_ARG, "plane range outside the owned planes");
     hipError_t e = launch_subsweep(c->G, d_disk, d_n, offset[0], offset[1], offset[2], sweep, c->stats, c->ovf,
-                                   c->stream);
+                                   zl_begin, zl_end, c->stream);
     return e == hipSuccess ? PMC_OK : hip_fail(e, "subsweep launch");
+}
+
+int pmc_subsweep(pmc_ctx* c, float* d_disk, const int16_t* d_n, const int offset[3], uint32_t sweep) {
+    if (!c) return fail(PMC_ERR_ARG, "null ctx");
+    return pmc_subsweep_range(c, d_disk, d_n, offset, sweep, 0, c->P.nz_local);
 }
 
 int pmc_shift_cells(pmc_ctx* c, const float* din, const int16_t* nin, float* dout, int16_t* nout, int f,
@@ -307,11 +315,16 @@ int pmc_init_lattice(pmc_ctx* c, int64_t n_atoms) {
     return pmc_assign(c, c->d_r, n_atoms, c->disk[c->cur], c->n[c->cur]);
 }
 
-int pmc_phase(pmc_ctx* c, int colour, uint32_t sweep) {
+int pmc_phase_range(pmc_ctx* c, int colour, uint32_t sweep, int zl_begin, int zl_end) {
     if (!c || colour < 0 || colour > 7) return fail(PMC_ERR_ARG, "bad argument");
     int o[3];
     pmc_colour_offset(colour, o);
-    return pmc_subsweep(c, c->disk[c->cur], c->n[c->cur], o, sweep);
+    return pmc_subsweep_range(c, c->disk[c->cur], c->n[c->cur], o, sweep, zl_begin, zl_end);
+}
+
+int pmc_phase(pmc_ctx* c, int colour, uint32_t sweep) {
+    if (!c) return fail(PMC_ERR_ARG, "null ctx");
+    return pmc_phase_range(c, colour, sweep, 0, c->P.nz_local);
 }
 
 int pmc_shift(pmc_ctx* c, uint32_t sweep) {

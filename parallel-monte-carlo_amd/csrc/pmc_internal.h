@@ -26,8 +26,10 @@ struct DevGeom {
 
 // Launchers (pmc_kernels.hip).  All asynchronous on `st`.
 // ovf: int[1 + cells_per_colour] scratch (overflow queue for the full-capacity fallback)
+// only cells in local planes [zl_begin, zl_end) of the colour are visited
 hipError_t launch_subsweep(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
-                           uint32_t sweep, unsigned long long* stats, int* ovf, hipStream_t st);
+                           uint32_t sweep, unsigned long long* stats, int* ovf, int zl_begin, int zl_end,
+                           hipStream_t st);
 int subsweep_capacity(const DevGeom& g);
 hipError_t launch_shift(const DevGeom& g, const float* din, const int16_t* nin, float* dout,
                         int16_t* nout, int f, float d, uint32_t* flags, hipStream_t st);

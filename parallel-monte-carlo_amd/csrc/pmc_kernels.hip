@@ -84,7 +84,7 @@ template <int NSLOT, int NMC>
 __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restrict__ disk,
                                               const int16_t* __restrict__ ncnt, int ox, int oy, int oz,
                                               uint32_t sweep, unsigned long long* __restrict__ stats,
-                                              float* __restrict__ px_, int cap, int t) {
+                                              float* __restrict__ px_, int cap, int t, int cz0) {
     constexpr int CPP = kWave / NSLOT;            // stencil cells staged per pass
     constexpr int NP = (26 + CPP - 1) / CPP;      // staging passes over the 26 neighbours
     const int lane = threadIdx.x & (kWave - 1);
@@ -95,7 +95,7 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     const int ncx = g.cps_x >> 1, ncy = g.cps_y >> 1;
     const int ta = wave_uniform(t % ncx);
     const int tb = wave_uniform((t / ncx) % ncy);
-    const int tc = wave_uniform(t / (ncx * ncy));
+    const int tc = cz0 + wave_uniform(t / (ncx * ncy));   // colour plane (z = 2*tc + oz)
     const int x = 2 * ta + ox, y = 2 * tb + oy, zl = 2 * tc + oz;
     const int zg0 = g.z0 + zl;
     const int plane = g.cps_x * g.cps_y;
@@ -331,7 +331,7 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep(DevGeom g, float
                                                                   const int16_t* __restrict__ ncnt,
                                                                   int ox, int oy, int oz, uint32_t sweep,
                                                                   unsigned long long* __restrict__ stats,
-                                                                  int cap, int* __restrict__ ovf) {
+                                                                  int cap, int* __restrict__ ovf, int cz0, int ncz) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform -> SALU math
     float* px_ = smem + wv * (3 * cap + kWave * g.ncache);
@@ -339,10 +339,10 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep(DevGeom g, float
     // XCD a contiguous run of cells -> neighbouring stencils share that XCD's L2.  Speed only.
     uint32_t nblk = gridDim.x, b = blockIdx.x;
     if ((nblk & 7u) == 0u) b = (b & 7u) * (nblk >> 3) + (b >> 3);
-    const int total = (g.cps_x >> 1) * (g.cps_y >> 1) * (g.nz_local >> 1);
+    const int total = (g.cps_x >> 1) * (g.cps_y >> 1) * ncz;
     const int t = (int)b * kSubWaves + wv;
     if (t >= total) return;
-    if (!subsweep_wave<NSLOT, NMC>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, cap, t)) {
+    if (!subsweep_wave<NSLOT, NMC>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, cap, t, cz0)) {
         if ((threadIdx.x & (kWave - 1)) == 0) ovf[1 + atomicAdd(&ovf[0], 1)] = t;
     }
 }
@@ -354,7 +354,7 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_fallback(DevGeom
                                                                            const int16_t* __restrict__ ncnt,
                                                                            int ox, int oy, int oz, uint32_t sweep,
                                                                            unsigned long long* __restrict__ stats,
-                                                                           int* __restrict__ ovf) {
+                                                                           int* __restrict__ ovf, int cz0) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int cap = 27 * (NMC > 0 ? NMC : g.nmax);
@@ -362,7 +362,7 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_fallback(DevGeom
     const int count = __builtin_amdgcn_readfirstlane(ovf[0]);
     for (int e = (int)blockIdx.x * kSubWaves + wv; e < count; e += (int)gridDim.x * kSubWaves) {
         const int t = __builtin_amdgcn_readfirstlane(ovf[1 + e]);
-        (void)subsweep_wave<NSLOT, NMC>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, cap, t);
+        (void)subsweep_wave<NSLOT, NMC>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, cap, t, cz0);
     }
 }
 
@@ -620,31 +620,40 @@ int subsweep_capacity(const DevGeom& g) {
 
 template <int NSLOT, int NMC>
 static void launch_subsweep_t(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
-                              uint32_t sweep, unsigned long long* stats, int* ovf, hipStream_t st) {
-    const int64_t total = (int64_t)(g.cps_x / 2) * (g.cps_y / 2) * (g.nz_local / 2);
+                              uint32_t sweep, unsigned long long* stats, int* ovf, int cz0, int ncz,
+                              hipStream_t st) {
+    const int64_t total = (int64_t)(g.cps_x / 2) * (g.cps_y / 2) * ncz;
     const int64_t blocks = (total + kSubWaves - 1) / kSubWaves;
     const int cap = subsweep_capacity(g);
     const int full = 27 * g.nmax;
     const size_t lds = sizeof(float) * (3 * (size_t)cap + kWave * (size_t)g.ncache) * kSubWaves;
     hipLaunchKernelGGL((k_subsweep<NSLOT, NMC>), dim3((unsigned)blocks), dim3(kWave * kSubWaves), lds, st, g,
-                       disk, n, ox, oy, oz, sweep, stats, cap, ovf);
+                       disk, n, ox, oy, oz, sweep, stats, cap, ovf, cz0, ncz);
     if (cap < full) {
         const size_t lds_full = sizeof(float) * (3 * (size_t)full + kWave * (size_t)g.ncache) * kSubWaves;
         hipLaunchKernelGGL((k_subsweep_fallback<NSLOT, NMC>), dim3(64), dim3(kWave * kSubWaves), lds_full, st,
-                           g, disk, n, ox, oy, oz, sweep, stats, ovf);
+                           g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0);
     }
 }
 
 hipError_t launch_subsweep(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
-                           uint32_t sweep, unsigned long long* stats, int* ovf, hipStream_t st) {
+                           uint32_t sweep, unsigned long long* stats, int* ovf, int zl_begin, int zl_end,
+                           hipStream_t st) {
+    // colour planes z = 2*cz + oz inside [zl_begin, zl_end)
+    auto ceil_half = [](int v) { return v <= 0 ? 0 : (v + 1) / 2; };
+    const int nczc = g.nz_local / 2;
+    int cz0 = ceil_half(zl_begin - oz), cz1 = ceil_half(zl_end - oz);
+    if (cz1 > nczc) cz1 = nczc;
+    if (cz1 <= cz0) return hipSuccess;
+    const int ncz = cz1 - cz0;
     hipError_t e = hipMemsetAsync(ovf, 0, sizeof(int), st);
     if (e != hipSuccess) return e;
-    if (g.nmax == 16) launch_subsweep_t<16, 16>(g, disk, n, ox, oy, oz, sweep, stats, ovf, st);
-    else if (g.nmax == 32) launch_subsweep_t<32, 32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, st);
-    else if (g.nslot == 8) launch_subsweep_t<8, 0>(g, disk, n, ox, oy, oz, sweep, stats, ovf, st);
-    else if (g.nslot == 16) launch_subsweep_t<16, 0>(g, disk, n, ox, oy, oz, sweep, stats, ovf, st);
-    else if (g.nslot == 32) launch_subsweep_t<32, 0>(g, disk, n, ox, oy, oz, sweep, stats, ovf, st);
-    else launch_subsweep_t<64, 0>(g, disk, n, ox, oy, oz, sweep, stats, ovf, st);
+    if (g.nmax == 16) launch_subsweep_t<16, 16>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st);
+    else if (g.nmax == 32) launch_subsweep_t<32, 32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st);
+    else if (g.nslot == 8) launch_subsweep_t<8, 0>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st);
+    else if (g.nslot == 16) launch_subsweep_t<16, 0>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st);
+    else if (g.nslot == 32) launch_subsweep_t<32, 0>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st);
+    else launch_subsweep_t<64, 0>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st);
     return hipGetLastError();
 }
 

@@ -102,6 +102,8 @@ def lib():
         _sig(L, "pmc_init_lattice", i32, _vp, i64)
         _sig(L, "pmc_sweep", i32, _vp, u32)
         _sig(L, "pmc_phase", i32, _vp, i32, u32)
+        _sig(L, "pmc_phase_range", i32, _vp, i32, u32, i32, i32)
+        _sig(L, "pmc_subsweep_range", i32, _vp, _vp, _vp, C.POINTER(C.c_int * 3), u32, i32, i32)
         _sig(L, "pmc_shift", i32, _vp, u32)
         _sig(L, "pmc_start", i32, _vp, u32, i32, C.POINTER(Result))
         _sig(L, "pmc_run_graph", i32, _vp, u32, i32)

@@ -117,6 +117,9 @@ class PmcContext:
     def phase(self, colour: int, s: int) -> None:
         check("pmc_phase", lib().pmc_phase(self._h, colour, s))
 
+    def phase_range(self, colour: int, s: int, zl_begin: int, zl_end: int) -> None:
+        check("pmc_phase_range", lib().pmc_phase_range(self._h, colour, s, zl_begin, zl_end))
+
     def shift(self, s: int) -> None:
         check("pmc_shift", lib().pmc_shift(self._h, s))
 

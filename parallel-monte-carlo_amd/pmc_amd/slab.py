@@ -59,19 +59,27 @@ class TorchP2P:
         self.world = world
         self.group = group
 
-    def exchange(self, sends: List[Tuple[object, int]], recvs: List[Tuple[object, int]]) -> None:
-        """sends/recvs: (tensor, peer).  Every rank issues its sends and receives in the same
-        logical order (down-plane first, then up-plane), which fixes the pairwise matching."""
+    def start(self, sends: List[Tuple[object, int]], recvs: List[Tuple[object, int]]):
+        """Issue the exchange; returns a handle for wait().  sends/recvs: (tensor, peer).  Every rank
+        issues its sends and receives in the same logical order (down-plane first, then up-plane),
+        which fixes the pairwise matching."""
         import torch.distributed as dist
         if self.world == 1:
             # periodic single-rank slab: each receive takes the send with the same role
             for (dst, _), (src, _) in zip(recvs, sends_for_self(sends, recvs)):
                 dst.copy_(src)
-            return
+            return []
         ops = [dist.P2POp(dist.isend, t, p, group=self.group) for t, p in sends]
         ops += [dist.P2POp(dist.irecv, t, p, group=self.group) for t, p in recvs]
-        for w in dist.batch_isend_irecv(ops):
+        return dist.batch_isend_irecv(ops)
+
+    @staticmethod
+    def wait(handle) -> None:
+        for w in handle or []:
             w.wait()
+
+    def exchange(self, sends, recvs) -> None:
+        self.wait(self.start(sends, recvs))
 
 
 def sends_for_self(sends, recvs):
@@ -141,7 +149,7 @@ class SlabSimulation:
         # counts travel as bytes: NCCL/RCCL has no 16-bit integer type
         return d, self.n[self.cur][z_local + 1].view(torch.uint8)
 
-    def _exchange(self, send_down: bool, send_up: bool, with_n: bool) -> None:
+    def _exchange(self, send_down: bool, send_up: bool, with_n: bool, wait: bool = True):
         g = self.g
         sends, recvs = [], []
         if send_down:   # my plane 0 -> top halo of the rank below; my top halo <- plane 0 of above
@@ -160,16 +168,25 @@ class SlabSimulation:
             if with_n:
                 sends.append((nn, g.above))
                 recvs.append((rn, g.below))
-        self._run(sends, recvs)
+        with self._on_stream():
+            handle = self.tp.start(sends, recvs)
+            if wait:
+                self.tp.wait(handle)
+                return None
+        return handle
 
-    def _run(self, sends, recvs):
+    def _wait(self, handle) -> None:
+        if handle:
+            with self._on_stream():
+                self.tp.wait(handle)
+
+    def _on_stream(self):
+        import contextlib
         stream = getattr(self, "stream", None)
-        if stream is not None:
-            import torch
-            with torch.cuda.stream(stream):
-                self.tp.exchange(sends, recvs)
-        else:
-            self.tp.exchange(sends, recvs)
+        if stream is None:
+            return contextlib.nullcontext()
+        import torch
+        return torch.cuda.stream(stream)
 
     def exchange_after_phase(self, colour: int) -> None:
         oz = colour % 2          # itoa (start.cu:153-157): offset[2] = colour % 2
@@ -189,17 +206,42 @@ class SlabSimulation:
         self.engine.shift(sweep)
         self.cur ^= 1
 
-    def sweep(self, s: int) -> None:
+    def sweep(self, s: int, timer=None) -> None:
+        """One sweep with communication hidden behind the halo-free interior.
+
+        Per colour: (1) the interior planes [1, nz-1) -- they read no halo -- run while the
+        previous exchange is in flight; (2) wait for it; (3) the two boundary planes; (4) start
+        sending the changed boundary plane without waiting.  shiftCells reads the halos, so it
+        waits; its own exchange overlaps the next sweep's first interior.  Cells of a colour are
+        independent, so the split does not change the result.  `timer(kind, fn)` wraps each launch
+        (kind "phase" or "shift").
+        """
+        run = timer or (lambda kind, fn: fn())
+        nz = self.g.nz
         order, _, _ = self.plan_fn(self.seed, s, self.w)
+        pending = getattr(self, "_pending", None)
         for colour in order:
-            self.phase_only(colour, s)
-            self.exchange_after_phase(colour)
-        self.shift_only(s)
-        self.exchange_after_shift()
+            run("phase", lambda: self.engine.phase_range(colour, s, 1, nz - 1))
+            self._wait(pending)
+            run("phase", lambda: self.engine.phase_range(colour, s, 0, 1))
+            if nz > 1:
+                run("phase", lambda: self.engine.phase_range(colour, s, nz - 1, nz))
+            oz = colour % 2
+            pending = self._exchange(send_down=(oz == 0), send_up=(oz == 1), with_n=False, wait=False)
+        self._wait(pending)
+        run("shift", lambda: self.engine.shift(s))
+        self.cur ^= 1
+        self._pending = self._exchange(True, True, with_n=True, wait=False)
+
+    def finish(self) -> None:
+        """Complete the outstanding halo exchange (call before reading the halos or the state)."""
+        self._wait(getattr(self, "_pending", None))
+        self._pending = None
 
     def run(self, first: int, count: int) -> None:
         for k in range(count):
             self.sweep(first + k)
+        self.finish()
 
     # ---- views ------------------------------------------------------------------------
     def owned(self):

@@ -24,6 +24,11 @@ class OracleEngine:
         pmc_oracle.lib().orc_subsweep(C.byref(self.p), self.d[self.cur], self.nn[self.cur], o[0], o[1], o[2],
                                       sweep, C.byref(self.stats))
 
+    def phase_range(self, colour, sweep, zl_begin, zl_end):
+        o = pmc_oracle.colour_offset(colour)
+        pmc_oracle.lib().orc_subsweep_range(C.byref(self.p), self.d[self.cur], self.nn[self.cur], o[0], o[1],
+                                            o[2], sweep, zl_begin, zl_end, C.byref(self.stats))
+
     def shift(self, sweep):
         _, f, d = pmc_oracle.sweep_plan(self.p.seed, sweep, self.p.w)
         over = pmc_oracle.lib().orc_shift_cells(C.byref(self.p), self.d[self.cur], self.nn[self.cur],
