@@ -375,47 +375,49 @@ __global__ __launch_bounds__(256) void k_shift(DevGeom g, const float* __restric
                                                const int16_t* __restrict__ nin, float* __restrict__ dout,
                                                int16_t* __restrict__ nout, int f, float d,
                                                uint32_t* __restrict__ flags) {
+    // grid: (ceil(cps_x / CPB), cps_y, nz_local); NSLOT lanes per cell, CPB cells per block along x
     constexpr int CPB = 256 / NSLOT;
     const int lane = threadIdx.x & (kWave - 1);
     const int p = threadIdx.x & (NSLOT - 1);
-    const int64_t t = (int64_t)blockIdx.x * CPB + threadIdx.x / NSLOT;
-    const int64_t total = (int64_t)g.cps_x * g.cps_y * g.nz_local;
-    const bool live = t < total;
+    const int x = (int)blockIdx.x * CPB + (int)(threadIdx.x / NSLOT);
+    const int y = (int)blockIdx.y, zl = (int)blockIdx.z;
+    const bool live = x < g.cps_x;
     const int nm = g.nmax;
     const float w = g.w;
 
-    int x = 0, y = 0, zl = 0;
-    if (live) {
-        x = (int)(t % g.cps_x);
-        y = (int)((t / g.cps_x) % g.cps_y);
-        zl = (int)(t / ((int64_t)g.cps_x * g.cps_y));
-    }
     const int cps_f = f == 0 ? g.cps_x : (f == 1 ? g.cps_y : g.cps_z);
     const float Lf = f == 0 ? g.Lx : (f == 1 ? g.Ly : g.Lz);
     const int dir = (d <= 0) ? -1 : 1;                     // shiftCells.h:46-53
     const float s = w * (float)dir;
-    const int cidf = f == 0 ? x : (f == 1 ? y : g.z0 + zl);
+    const int xx = live ? x : 0;
+    const int cidf = f == 0 ? xx : (f == 1 ? y : g.z0 + zl);
     const float offset = (float)cidf * w - Lf / 2.0f;     // :55
     int nbg = cidf + dir;
     if (nbg < 0) nbg = cps_f - 1; else if (nbg >= cps_f) nbg = 0;
-    int nx = x, ny = y, nz = zl;
+    int nx = xx, ny = y, nz = zl;
     if (f == 0) nx = nbg; else if (f == 1) ny = nbg; else nz = g.halo ? zl + dir : nbg;
     const float offset_nb = (float)nbg * w - Lf / 2.0f;
-    const int64_t c = sidx(g, x, y, zl);
-    const int64_t cnb = sidx(g, nx, ny, nz);
+    const uint32_t plane = (uint32_t)g.cps_x * (uint32_t)g.cps_y;
+    const uint32_t c = (uint32_t)xx + (uint32_t)g.cps_x * (uint32_t)y + plane * (uint32_t)(zl + g.halo);
+    const uint32_t cnb = (uint32_t)nx + (uint32_t)g.cps_x * (uint32_t)ny + plane * (uint32_t)(nz + g.halo);
 
-    int ncur = 0, nnb = 0;
-    if (live) { ncur = nin[c]; nnb = nin[cnb]; }
-    float D = 0.0f, Dn = 0.0f;
-    bool keep = false, take = false;
-    if (p < ncur) {
-        D = (din[c * 3 * nm + f * nm + p] - offset) - d;   // shortDisk - d
-        keep = D > 0 && D <= w;
+    // one round trip: both counts and all six rows (a 64 B row sits inside one 128 B line)
+    const int ncur = live ? nin[c] : 0;
+    const int nnb = live ? nin[cnb] : 0;
+    const int pp = p < nm ? p : 0;
+    const uint32_t oc = c * (uint32_t)(3 * nm) + (uint32_t)pp, on = cnb * (uint32_t)(3 * nm) + (uint32_t)pp;
+    float own[3], nbv[3];
+#pragma unroll
+    for (int dim = 0; dim < 3; ++dim) {
+        own[dim] = din[oc + (uint32_t)(dim * nm)];
+        nbv[dim] = din[on + (uint32_t)(dim * nm)];
     }
-    if (p < nnb) {
-        Dn = (din[cnb * 3 * nm + f * nm + p] - offset_nb) - d;
-        take = !(Dn > 0 && Dn <= w);
-    }
+    const float xf = f == 0 ? own[0] : (f == 1 ? own[1] : own[2]);
+    const float xfn = f == 0 ? nbv[0] : (f == 1 ? nbv[1] : nbv[2]);
+    const float D = (xf - offset) - d;                    // shortDisk - d
+    const float Dn = (xfn - offset_nb) - d;
+    const bool keep = (p < ncur) && (D > 0 && D <= w);
+    const bool take = (p < nnb) && !(Dn > 0 && Dn <= w);
     const unsigned long long bk = __ballot(keep);
     const unsigned long long bt = __ballot(take);
     const int gsh = lane & ~(NSLOT - 1);
@@ -425,12 +427,13 @@ __global__ __launch_bounds__(256) void k_shift(DevGeom g, const float* __restric
     const unsigned long long below = (1ull << p) - 1ull;
     const int nk = __popcll(km);
     const int nnew = nk + __popcll(tm);
+    const uint32_t ob = c * (uint32_t)(3 * nm);
     if (keep) {
         const int dst = __popcll(km & below);
         if (dst < nm) {
 #pragma unroll
             for (int dim = 0; dim < 3; ++dim)
-                dout[c * 3 * nm + dim * nm + dst] = (dim == f) ? D + offset : din[c * 3 * nm + dim * nm + p];
+                dout[ob + (uint32_t)(dim * nm + dst)] = (dim == f) ? D + offset : own[dim];
         }
     }
     if (take) {
@@ -438,8 +441,7 @@ __global__ __launch_bounds__(256) void k_shift(DevGeom g, const float* __restric
         if (dst < nm) {
 #pragma unroll
             for (int dim = 0; dim < 3; ++dim)
-                dout[c * 3 * nm + dim * nm + dst] =
-                    (dim == f) ? ((Dn + offset) + s) : din[cnb * 3 * nm + dim * nm + p];
+                dout[ob + (uint32_t)(dim * nm + dst)] = (dim == f) ? ((Dn + offset) + s) : nbv[dim];
         }
     }
     if (live && p == 0) {
@@ -659,9 +661,8 @@ hipError_t launch_subsweep(const DevGeom& g, float* disk, const int16_t* n, int 
 
 hipError_t launch_shift(const DevGeom& g, const float* din, const int16_t* nin, float* dout,
                         int16_t* nout, int f, float d, uint32_t* flags, hipStream_t st) {
-    const int64_t total = (int64_t)g.cps_x * g.cps_y * g.nz_local;
     const int cpb = 256 / g.nslot;
-    dim3 grid((unsigned)((total + cpb - 1) / cpb)), block(256);
+    dim3 grid((unsigned)((g.cps_x + cpb - 1) / cpb), (unsigned)g.cps_y, (unsigned)g.nz_local), block(256);
     switch (g.nslot) {
         case 8: hipLaunchKernelGGL(k_shift<8>, grid, block, 0, st, g, din, nin, dout, nout, f, d, flags); break;
         case 16: hipLaunchKernelGGL(k_shift<16>, grid, block, 0, st, g, din, nin, dout, nout, f, d, flags); break;

@@ -231,3 +231,21 @@ def test_mean_energy_known_answer(oracle):
     blocks = es.reshape(20, -1).mean(1)
     se = blocks.std(ddof=1) / np.sqrt(len(blocks))
     assert abs(es.mean() - (-21.240)) < 3 * math.hypot(se, 0.022) + 0.02
+
+
+def test_subsweep_range_split_equals_full(oracle):
+    """A colour phase split into plane ranges (interior first, then boundaries -- the slab
+    driver's order) equals the unsplit phase: cells of one colour are independent."""
+    import ctypes as C
+    a = oracle.OracleState(oracle.make_params(cps=8))
+    b = oracle.OracleState(oracle.make_params(cps=8))
+    a.init_lattice(2000)
+    b.init_lattice(2000)
+    for colour in (0, 3, 5, 6):
+        o = oracle.colour_offset(colour)
+        a.subsweep(o, 7)
+        for lo, hi in ((1, 7), (0, 1), (7, 8)):
+            oracle.lib().orc_subsweep_range(C.byref(b.p), b.disk, b.n, o[0], o[1], o[2], 7, lo, hi,
+                                            C.byref(b.stats))
+    assert np.array_equal(a.disk, b.disk)
+    assert a.stats.as_dict() == b.stats.as_dict()
