@@ -190,6 +190,21 @@ PMC_HD float pmc_lj4_from_r2(float r2, float rc2) {
 
 PMC_HD float pmc_lj_from_r2(float r2, float rc2) { return 4.0f * pmc_lj4_from_r2(r2, rc2); }
 
+/* Signed quarter pair energy of a listed term (the caller has already applied the cutoff):
+ * r2s = +r2 for a new-position term, -r2 for an old-position term (sign bit set, -0 included).
+ * Returns +u(r2) resp. -u(r2) bit for bit, u as in pmc_lj4_from_r2: round-to-nearest is
+ * symmetric, so (inv*inv)*(-inv) = -p6 and (-p6)*p6 - (-p6) = -(p6*p6 - p6) exactly.  Costs one
+ * bit-select over the unsigned form (|r2s| and |p6s| are free source modifiers on gfx950). */
+PMC_HD float pmc_lj4_signed_m(float r2s, float r2min) {   /* r2min == PMC_R2_MIN */
+    float a = __builtin_fabsf(r2s);
+    float rr = a < r2min ? r2min : a;   /* = fmaxf for non-NaN; one compare + select, no canonicalize */
+    float inv = pmc_recip(rr);
+    float invs = __builtin_copysignf(inv, r2s);
+    float p6s = (inv * inv) * invs;
+    return p6s * __builtin_fabsf(p6s) - p6s;
+}
+PMC_HD float pmc_lj4_signed(float r2s) { return pmc_lj4_signed_m(r2s, PMC_R2_MIN); }
+
 /* Conservative partner filter (staging): squared distance from a staged partner to the own
  * cell's closed box [lo, hi] (each side padded by PMC_BOX_PAD).  A partner with
  * d2 > rc2 * (1 + 2^-13) is farther than the cutoff from every position a particle of the cell

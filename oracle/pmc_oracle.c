@@ -237,29 +237,32 @@ static void subsweep_cell(const pmc_params* p, float* disk, const int16_t* n, in
         int out = (ddx > hw) || (ddx < -hw) || (ddy > hw) || (ddy < -hw) || (ddz > hw) || (ddz < -hw);
         if (!out) {
             ++*ev;
-            /* energies (calculate_old/new_energy, subsweep.h:175-191).  Partner k (neighbours
-             * first, own cell after) runs on wave lane k%64, passes in ascending k.  Per lane:
-             * newp/oldp = neighbour new/old energy partials, down = own-cell (e_new - e_old);
-             * v = down + (newp - oldp); dE = xor butterfly 1,2,...,32 over the 64 lanes.
-             * (The kernel caches a particle's old partials after its first move; a recomputed
-             * old energy at the accepted position is bitwise its cached new energy, so the
-             * oracle simply recomputes.) */
-            float newp[64], oldp[64], down[64];
-            for (int l = 0; l < 64; ++l) { newp[l] = 0.0f; oldp[l] = 0.0f; down[l] = 0.0f; }
-            for (int k = 0; k < K; ++k) {
-                const int l = k & 63;
-                const float xj = px_[k], yj = py_[k], zj = pz_[k];
-                const float en = pmc_lj_from_r2(pmc_r2(qx - xj, qy - yj, qz - zj), rc2);
-                const float eo = pmc_lj_from_r2(pmc_r2(xi - xj, yi - yj, zi - zj), rc2);
-                if (k < S_nb) {
-                    newp[l] = newp[l] + en;
-                    oldp[l] = oldp[l] + eo;
-                } else if (k - S_nb != i) {
-                    down[l] = down[l] + (en - eo);
+            /* energies (calculate_old/new_energy, subsweep.h:175-191): dE = sum over partners
+             * k != i of e(new) - e(old).  Term list (the kernel's compaction, spec v6): for each
+             * block of 64 staged partners (neighbours first, own cell after) append the new
+             * terms with r2 <= rc2 in ascending k, then the old terms with r2 <= rc2 in
+             * ascending k (pairs beyond the cutoff are exactly 0 and are not listed).  Term t is
+             * summed by lane t%64 in ascending t as +u (new) / -u (old), u the quarter energy;
+             * v = 4 * lane sum; dE = xor butterfly 1,2,...,32 over the 64 lanes. */
+            float part[64];
+            for (int l = 0; l < 64; ++l) part[l] = 0.0f;
+            int t = 0;
+            for (int base = 0; base < K; base += 64) {
+                const int kend = base + 64 < K ? base + 64 : K;
+                for (int pass = 0; pass < 2; ++pass) {
+                    const float sx = pass ? xi : qx, sy = pass ? yi : qy, sz = pass ? zi : qz;
+                    for (int k = base; k < kend; ++k) {
+                        if (k == S_nb + i) continue;
+                        const float r2 = pmc_r2(sx - px_[k], sy - py_[k], sz - pz_[k]);
+                        if (r2 <= rc2) {
+                            part[t & 63] = part[t & 63] + pmc_lj4_signed(pass ? -r2 : r2);
+                            ++t;
+                        }
+                    }
                 }
             }
             float lane[64];
-            for (int l = 0; l < 64; ++l) lane[l] = down[l] + (newp[l] - oldp[l]);
+            for (int l = 0; l < 64; ++l) lane[l] = 4.0f * part[l];
             for (int mask = 1; mask < 64; mask <<= 1) {
                 float t[64];
                 for (int l = 0; l < 64; ++l) t[l] = lane[l] + lane[l ^ mask];

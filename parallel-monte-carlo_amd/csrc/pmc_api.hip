@@ -95,9 +95,7 @@ DevGeom make_geom(const pmc_params& p) {
     g.Lz = (float)p.cps_z * p.w;
     g.rc2 = pmc_cutoff_r2(p.w);
     g.rc2f = pmc_filter_r2(g.rc2);
-    // a slot's old-energy partials are reused only if the slot moves again in the same visit:
-    // slot i < n_own with i + n_own < n_moves, hence i < n_moves / 2 (and < nmax)
-    g.ncache = p.n_moves / 2 < p.nmax ? p.n_moves / 2 : p.nmax;
+    g.r2min = PMC_R2_MIN;
     g.k0 = (uint32_t)p.seed;
     g.k1 = (uint32_t)(p.seed >> 32);
     return g;

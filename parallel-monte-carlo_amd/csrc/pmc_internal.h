@@ -12,15 +12,18 @@ namespace pmc {
 constexpr int kWave = 64;          // CDNA wavefront
 constexpr int kSubWaves = 4;       // cells (waves) per subsweep workgroup
 constexpr int kStatSlots = 1024;   // stats accumulator slots per counter (contention spread)
+// subsweep LDS per wave: x, y, z rows of `stride` partner slots + a term list of 2*stride + 64
+__host__ __device__ constexpr int lds_floats_per_wave(int stride) { return 5 * stride + 64; }
+constexpr int kMainStride = 240;    // main launch: lds_floats_per_wave(240) * 4 B = 5056 B <= 5 KiB
 constexpr int kStatCounters = 4;   // de_fixed, accepted, trials, evaluated
 
 // Flattened kernel parameters (passed by value).
 struct DevGeom {
     int cps_x, cps_y, cps_z, nz_local, z0, halo, nmax, n_moves;
     int nslot;                     // power of two >= nmax (lanes per cell in shift/energy)
-    int ncache;                    // own slots with cached old-energy partials: min(nmax, n_moves)
     float w, beta, sigma, Lx, Ly, Lz, rc2;
     float rc2f;                    // staging filter threshold (pmc_filter_r2)
+    float r2min;                   // PMC_R2_MIN (passed as data so the kernel keeps it in an SGPR)
     uint32_t k0, k1;
 };
 

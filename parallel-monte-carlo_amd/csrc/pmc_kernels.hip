@@ -6,9 +6,9 @@
 //   * the cell's 27-cell stencil (own cell first, shuffled; then the 26 neighbours in
 //     get_neighbors order, subsweep.h:119-137) is staged once into LDS (SoA x/y/z), with the
 //     periodic image (apply_PBC, subsweep.h:139-151) folded into the staged coordinates;
-//   * per trial move every lane evaluates old and new pair energies of its partners
-//     (lane = partner index mod 64) and the wave reduces dE with DPP / swizzle (no LDS, no
-//     barrier); accept/reject is wave-uniform and in-kernel;
+//   * per trial move the lanes test old and new distances of the partners (lane = partner index
+//     mod 64), evaluate the pair energies of the compacted in-cutoff pairs, and the wave reduces
+//     dE with DPP / permlane (no barrier); accept/reject is wave-uniform and in-kernel;
 //   * Philox4x32-10 counter slots give every (sweep, cell, move) its own random numbers, so
 //     results are independent of launch geometry and identical to the CPU oracle.
 // No MFMA: this is not a dense contraction (pair energies are gathered, cut-off, divided).
@@ -35,10 +35,10 @@ __device__ __forceinline__ int as_i(float v) { return __builtin_bit_cast(int, v)
 // operands = v the swapped pair holds (own, partner) and their sum is the butterfly step in every
 // lane (float add is commutative, so both lanes of a pair get identical bits).  No LDS, no SGPR.
 __device__ __forceinline__ float wave_sum_fixed_order(float v) {
-    v = v + as_f(__builtin_amdgcn_mov_dpp(as_i(v), 0xB1, 0xF, 0xF, false));   // quad_perm 1,0,3,2
-    v = v + as_f(__builtin_amdgcn_mov_dpp(as_i(v), 0x4E, 0xF, 0xF, false));   // quad_perm 2,3,0,1
-    v = v + as_f(__builtin_amdgcn_mov_dpp(as_i(v), 0x141, 0xF, 0xF, false));  // row_half_mirror
-    v = v + as_f(__builtin_amdgcn_mov_dpp(as_i(v), 0x140, 0xF, 0xF, false));  // row_mirror
+    v = v + as_f(__builtin_amdgcn_update_dpp(0, as_i(v), 0xB1, 0xF, 0xF, true));   // quad_perm 1,0,3,2
+    v = v + as_f(__builtin_amdgcn_update_dpp(0, as_i(v), 0x4E, 0xF, 0xF, true));   // quad_perm 2,3,0,1
+    v = v + as_f(__builtin_amdgcn_update_dpp(0, as_i(v), 0x141, 0xF, 0xF, true));  // row_half_mirror
+    v = v + as_f(__builtin_amdgcn_update_dpp(0, as_i(v), 0x140, 0xF, 0xF, true));  // row_mirror
     {
         const auto r = __builtin_amdgcn_permlane16_swap((unsigned)as_i(v), (unsigned)as_i(v), false, false);
         v = as_f((int)r[0]) + as_f((int)r[1]);                                // xor 16
@@ -51,6 +51,12 @@ __device__ __forceinline__ float wave_sum_fixed_order(float v) {
 }
 
 __device__ __forceinline__ int wave_uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// number of set bits of the 64-lane mask m below this lane (+ add)
+__device__ __forceinline__ int mbcnt64_add(unsigned long long m, int add) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, (uint32_t)add));
+}
+__device__ __forceinline__ int mbcnt64(unsigned long long m) { return mbcnt64_add(m, 0); }
 
 // storage index of local cell (x, y, zl)
 __device__ __forceinline__ int64_t sidx(const DevGeom& g, int x, int y, int zl) {
@@ -71,27 +77,30 @@ __device__ __forceinline__ int64_t sidx(const DevGeom& g, int x, int y, int zl) 
 //   3. stage the neighbours into LDS, keeping (ballot + mbcnt compaction) only partners within
 //      the cutoff of the own cell's box -- the others contribute exactly 0 -- then the own cell
 //      (shuffled) after them;
-//   4. n_M moves: lane l evaluates partners k = l + 64*pass; a particle's neighbour old-energy
-//      partials are kept per lane in LDS after its first move (neighbours are static in a phase
-//      and a recomputation would give the same bits), so later moves evaluate only new energies;
-//      one fixed-order DPP/permlane reduction gives dE; accept in-kernel, wave-uniformly;
+//   4. n_M moves: per block of 64 partners, lane l computes the new- and old-position r2 of
+//      partner 64*block + l; the pairs within the cutoff (about 1 in 5) are compacted by
+//      ballot + mbcnt into an LDS term list (new terms, then old terms with the sign bit set),
+//      and only those reach the reciprocal -- term t on lane t % 64; one fixed-order
+//      DPP/permlane reduction gives dE; accept in-kernel, wave-uniformly;
 //   5. write back the own cell; one atomic per counter per wave.
-// LDS per wave: 3 * 27*nmax floats (partners) + 64 * ncache floats (old-energy partials).
+// LDS per wave: x, y, z rows of `stride` partner slots, then the term list (2 * stride + 64
+// floats; the extra 64 let a pass read a full 64-lane block without clamping).
 // ------------------------------------------------------------------------------------------
 // Returns false (and leaves the cell untouched) when the cell's staged partners do not fit the
 // LDS capacity `cap`; the caller queues it for the full-capacity fallback launch.
-template <int NSLOT, int NMC>
+template <int NSLOT, int NMC, int STRIDE>
 __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restrict__ disk,
                                               const int16_t* __restrict__ ncnt, int ox, int oy, int oz,
                                               uint32_t sweep, unsigned long long* __restrict__ stats,
-                                              float* __restrict__ px_, int cap, int t, int cz0) {
+                                              float* __restrict__ px_, int stride_rt, int cap, int t,
+                                              int cz0) {
     constexpr int CPP = kWave / NSLOT;            // stencil cells staged per pass
     constexpr int NP = (26 + CPP - 1) / CPP;      // staging passes over the 26 neighbours
     const int lane = threadIdx.x & (kWave - 1);
     const int nm = NMC > 0 ? NMC : g.nmax;        // compile-time for the common nmax
-    float* py_ = px_ + cap;
-    float* pz_ = py_ + cap;
-    float* cache = pz_ + cap;
+    const int stride = STRIDE > 0 ? STRIDE : stride_rt;   // compile-time -> LDS offset immediates
+    float* py_ = px_ + stride;
+    float* pz_ = py_ + stride;
     const int ncx = g.cps_x >> 1, ncy = g.cps_y >> 1;
     const int ta = wave_uniform(t % ncx);
     const int tb = wave_uniform((t / ncx) % ncy);
@@ -161,8 +170,8 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
         const float R = __builtin_sqrtf(-2.0f * lg);
         float sn, cs;
         pmc_det_sincos_2pi(pmc_u01(ws), &sn, &cs);
-        G0 = R * cs;      // lanes 0-15: g0 of move m0+lane; lanes 32-47: g2 of move m0+lane-32
-        G1 = R * sn;      // lanes 0-15: g1
+        G0 = (R * cs) * g.sigma;   // lanes 0-15: g0*sigma of move m0+lane; 32-47: g2*sigma
+        G1 = (R * sn) * g.sigma;   // lanes 0-15: g1*sigma
         TT = -lg;         // lanes 16-31: acceptance threshold of move m0+lane-16
     };
     rng_chunk(0, true);
@@ -199,8 +208,7 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
         const float uz = vz[q] + __shfl(k_sz, ks);
         const bool keep = (k < 27) && (p < cnt) && (pmc_box_d2(ux, uy, uz, blo, bhi) <= g.rc2f);
         const unsigned long long mk = __ballot(keep);
-        const int dst = S_nb + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
-                                           __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+        const int dst = S_nb + mbcnt64(mk);
         if (keep && dst < cap_nb) {
             px_[dst] = ux;
             py_[dst] = uy;
@@ -228,9 +236,11 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     const float czf = (float)zg0 * g.w - g.Lz / 2.0f + hw;
     const double beta_d = (double)g.beta;
     const float rc2 = g.rc2;
-    const int ncache = g.ncache;
+    float* buf = pz_ + stride;                  // term list: signed r2 values
+    // PMC_R2_MIN through an SGPR: v_max_f32 |r2s|, s takes it with the free |.| modifier (a
+    // literal operand would force a second max)
+    const float r2min = as_f(wave_uniform(as_i(g.r2min)));
 
-    uint64_t cvalid = 0;
     double de_cell = 0.0;
     int n_acc = 0, n_ev = 0;
     int i = 0;
@@ -239,67 +249,64 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
         if (m0 > 0) rng_chunk(m0, false);
         const int mend = (g.n_moves - m0) < 16 ? (g.n_moves - m0) : 16;
         for (int ml = 0; ml < mend; ++ml) {
-            const float g0 = as_f(__builtin_amdgcn_readlane(as_i(G0), ml));
-            const float g1 = as_f(__builtin_amdgcn_readlane(as_i(G1), ml));
-            const float g2 = as_f(__builtin_amdgcn_readlane(as_i(G0), 32 + ml));
+            const float d0 = as_f(__builtin_amdgcn_readlane(as_i(G0), ml));
+            const float d1 = as_f(__builtin_amdgcn_readlane(as_i(G1), ml));
+            const float d2 = as_f(__builtin_amdgcn_readlane(as_i(G0), 32 + ml));
             const float Tm = as_f(__builtin_amdgcn_readlane(as_i(TT), 16 + ml));
             const int si = S_nb + i;
             const float xi = px_[si], yi = py_[si], zi = pz_[si];
-            const float qx = xi + g0 * g.sigma;
-            const float qy = yi + g1 * g.sigma;
-            const float qz = zi + g2 * g.sigma;
+            const float qx = xi + d0;                  // make_move: x + g * sigma
+            const float qy = yi + d1;
+            const float qz = zi + d2;
             const float ddx = qx - cxf, ddy = qy - cyf, ddz = qz - czf;
             // (d > hw || d < -hw) == (|d| > hw) for non-NaN d; |d| is a free source modifier
             const bool out = (__builtin_fabsf(ddx) > hw) || (__builtin_fabsf(ddy) > hw) ||
                              (__builtin_fabsf(ddz) > hw);
             if (!out) {
                 ++n_ev;
-                const bool cached = (cvalid >> i) & 1ull;
-                float newp = 0.0f, oldp = 0.0f, down = 0.0f;
-                int k0p = 0;
-                // passes entirely inside the neighbour list: no own-cell bookkeeping
-                if (cached) {   // new energies only (old partials come from the cache)
-                    for (; k0p + kWave <= S_nb; k0p += kWave) {
-                        const int k = k0p + lane;
-                        const float xj = px_[k], yj = py_[k], zj = pz_[k];
-                        newp = newp + pmc_lj4_from_r2(pmc_r2(qx - xj, qy - yj, qz - zj), rc2);
-                    }
-                } else {
-                    for (; k0p + kWave <= S_nb; k0p += kWave) {
-                        const int k = k0p + lane;
-                        const float xj = px_[k], yj = py_[k], zj = pz_[k];
-                        newp = newp + pmc_lj4_from_r2(pmc_r2(qx - xj, qy - yj, qz - zj), rc2);
-                        oldp = oldp + pmc_lj4_from_r2(pmc_r2(xi - xj, yi - yj, zi - zj), rc2);
-                    }
+                // 4a. term list: per block of 64 partners, the new-position terms within the
+                // cutoff, then the old-position ones (sign bit set), compacted by ballot+mbcnt.
+                // ~80% of staged pairs lie beyond rc for a given position; they are exactly 0
+                // and never reach the reciprocal.
+                int C = 0;   // wave-uniform
+                for (int base = 0; base < K; base += kWave) {
+                    // no clamp: slots in [K, base + 64) are inside this wave's LDS (stride >= 64
+                    // past the x row start, term list padded by 64) and are masked by `ok`
+                    const int k = base + lane;
+                    const float xj = px_[k], yj = py_[k], zj = pz_[k];
+                    const float r2n = pmc_r2(qx - xj, qy - yj, qz - zj);
+                    const float r2o = pmc_r2(xi - xj, yi - yj, zi - zj);
+                    // lanes past K and the moving particle's own slot are masked in SALU
+                    const int rem = K - base;
+                    unsigned long long okm = rem >= kWave ? ~0ull : ((1ull << rem) - 1ull);
+                    const int sr = si - base;
+                    if (sr >= 0 && sr < kWave) okm &= ~(1ull << sr);
+                    const unsigned long long mn = __builtin_amdgcn_ballot_w64(r2n <= rc2) & okm;
+                    const unsigned long long mo = __builtin_amdgcn_ballot_w64(r2o <= rc2) & okm;
+                    const int cn = C + __popcll(mn);
+                    // wave-uniform list heads (SGPR addresses; mbcnt's addend would need a VGPR)
+                    float* hn = buf + C;
+                    float* ho = buf + cn;
+                    if (__builtin_amdgcn_inverse_ballot_w64(mn)) hn[mbcnt64(mn)] = r2n;
+                    if (__builtin_amdgcn_inverse_ballot_w64(mo)) ho[mbcnt64(mo)] = -r2o;
+                    C = cn + __popcll(mo);
                 }
-                // tail pass(es): the rest of the neighbours + the own cell
-                for (; k0p < K; k0p += kWave) {
-                    const int k = k0p + lane;
-                    const int kr = k < K ? k : 0;
-                    const float xj = px_[kr], yj = py_[kr], zj = pz_[kr];
-                    const float en = pmc_lj4_from_r2(pmc_r2(qx - xj, qy - yj, qz - zj), rc2);
-                    const float eo = pmc_lj4_from_r2(pmc_r2(xi - xj, yi - yj, zi - zj), rc2);
-                    const bool is_nb = k < S_nb;
-                    const bool is_own = (k >= S_nb) && (k < K) && (k - S_nb != i);
-                    newp = newp + (is_nb ? en : 0.0f);
-                    oldp = oldp + ((is_nb && !cached) ? eo : 0.0f);
-                    down = down + (is_own ? (en - eo) : 0.0f);
+                // 4b. energies of the listed terms: term t on lane t % 64, ascending t
+                float acc = 0.0f;
+                for (int t0 = 0; t0 < C; t0 += kWave) {
+                    const int tt = t0 + lane;
+                    const float us = pmc_lj4_signed_m(buf[tt], r2min);   // buf padded: no clamp
+                    acc = acc + (tt < C ? us : 0.0f);
                 }
-                if (cached) oldp = cache[i * kWave + lane];
                 // quarter energies were accumulated; the factor 4 is exact, so 4*(sum of u)
                 // equals the sum of the 4u the oracle accumulates, bit for bit
-                const float v = 4.0f * (down + (newp - oldp));
-                const float dE = wave_sum_fixed_order(v);
-                const bool accept = beta_d * (double)dE < (double)Tm;   // accept_move, subsweep.h:209-216
-                // keep the partials only if slot i moves again in this visit and fits the cache
-                if (i < ncache && (accept || !cached)) {
-                    cache[i * kWave + lane] = accept ? newp : oldp;
-                    cvalid |= 1ull << i;
-                }
-                if (accept) {
+                const float dE = wave_sum_fixed_order(4.0f * acc);
+                // dE is wave-uniform (every lane holds the butterfly total): make that explicit
+                const float dEu = as_f(__builtin_amdgcn_readfirstlane(as_i(dE)));
+                if (beta_d * (double)dEu < (double)Tm) {               // accept_move, subsweep.h:209-216
                     if (lane == 0) { px_[si] = qx; py_[si] = qy; pz_[si] = qz; }
                     ++n_acc;
-                    de_cell = de_cell + (double)dE;
+                    de_cell = de_cell + (double)dEu;
                 }
             }
             i += 1;
@@ -324,8 +331,9 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     return true;
 }
 
-// Main launch: one wave per cell of the colour; LDS capacity `cap` partners per wave (sized for
-// the occupancy; a cell whose filtered stencil exceeds it is queued in ovf for the fallback).
+// Main launch: one wave per cell of the colour; LDS layout stride kMainStride, capacity `cap`
+// (<= kMainStride) partners per wave (sized for the occupancy; a cell whose filtered stencil
+// exceeds it is queued in ovf for the fallback).
 template <int NSLOT, int NMC>
 __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep(DevGeom g, float* __restrict__ disk,
                                                                   const int16_t* __restrict__ ncnt,
@@ -334,7 +342,7 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep(DevGeom g, float
                                                                   int cap, int* __restrict__ ovf, int cz0, int ncz) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform -> SALU math
-    float* px_ = smem + wv * (3 * cap + kWave * g.ncache);
+    float* px_ = smem + wv * lds_floats_per_wave(kMainStride);
     // XCD-aware block order: blocks b and b+8 share an XCD (round-robin dispatch), so give each
     // XCD a contiguous run of cells -> neighbouring stencils share that XCD's L2.  Speed only.
     uint32_t nblk = gridDim.x, b = blockIdx.x;
@@ -342,7 +350,8 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep(DevGeom g, float
     const int total = (g.cps_x >> 1) * (g.cps_y >> 1) * ncz;
     const int t = (int)b * kSubWaves + wv;
     if (t >= total) return;
-    if (!subsweep_wave<NSLOT, NMC>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, cap, t, cz0)) {
+    if (!subsweep_wave<NSLOT, NMC, kMainStride>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, kMainStride, cap,
+                                                t, cz0)) {
         if ((threadIdx.x & (kWave - 1)) == 0) ovf[1 + atomicAdd(&ovf[0], 1)] = t;
     }
 }
@@ -357,12 +366,13 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_fallback(DevGeom
                                                                            int* __restrict__ ovf, int cz0) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int cap = 27 * (NMC > 0 ? NMC : g.nmax);
-    float* px_ = smem + wv * (3 * cap + kWave * g.ncache);
+    const int full = 27 * (NMC > 0 ? NMC : g.nmax);
+    float* px_ = smem + wv * lds_floats_per_wave(full);
     const int count = __builtin_amdgcn_readfirstlane(ovf[0]);
     for (int e = (int)blockIdx.x * kSubWaves + wv; e < count; e += (int)gridDim.x * kSubWaves) {
         const int t = __builtin_amdgcn_readfirstlane(ovf[1 + e]);
-        (void)subsweep_wave<NSLOT, NMC>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, cap, t, cz0);
+        (void)subsweep_wave<NSLOT, NMC, 27 * NMC>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, full, full, t,
+                                                  cz0);
     }
 }
 
@@ -606,8 +616,9 @@ __global__ void k_selftest(const uint32_t* __restrict__ words, int count, float*
 // ------------------------------------------------------------------------------------------
 int subsweep_capacity(const DevGeom& g) {
     // Partners per wave held in LDS by the main launch.  Sized so a wave needs at most 5 KiB of
-    // LDS (-> 32 waves/CU, the hardware limit): 3 floats per partner + 64 floats per cache slot.
-    // The filtered stencil holds ~98 partners at n = 4.77 per cell; larger ones use the fallback.
+    // LDS (-> 32 waves/CU, the hardware limit): 3 floats per partner (x, y, z) + 2 term-list
+    // entries + 64 (kMainStride = 240).  The filtered stencil holds ~98 partners at n = 4.77 per
+    // cell; larger ones use the fallback.
     const int full = 27 * g.nmax;
     // test hook: PMC_SUBSWEEP_CAP forces a (small) capacity so the fallback path is exercised
     static const int forced = [] {
@@ -615,9 +626,7 @@ int subsweep_capacity(const DevGeom& g) {
         return e ? std::atoi(e) : 0;
     }();
     if (forced > 0) return forced < full ? forced : full;
-    const int cap = (5120 / 4 - kWave * g.ncache) / 3;
-    if (cap < 128) return full;
-    return cap < full ? cap : full;
+    return kMainStride < full ? kMainStride : full;
 }
 
 template <int NSLOT, int NMC>
@@ -628,11 +637,11 @@ static void launch_subsweep_t(const DevGeom& g, float* disk, const int16_t* n, i
     const int64_t blocks = (total + kSubWaves - 1) / kSubWaves;
     const int cap = subsweep_capacity(g);
     const int full = 27 * g.nmax;
-    const size_t lds = sizeof(float) * (3 * (size_t)cap + kWave * (size_t)g.ncache) * kSubWaves;
+    const size_t lds = sizeof(float) * (size_t)lds_floats_per_wave(kMainStride) * kSubWaves;
     hipLaunchKernelGGL((k_subsweep<NSLOT, NMC>), dim3((unsigned)blocks), dim3(kWave * kSubWaves), lds, st, g,
                        disk, n, ox, oy, oz, sweep, stats, cap, ovf, cz0, ncz);
     if (cap < full) {
-        const size_t lds_full = sizeof(float) * (3 * (size_t)full + kWave * (size_t)g.ncache) * kSubWaves;
+        const size_t lds_full = sizeof(float) * (size_t)lds_floats_per_wave(full) * kSubWaves;
         hipLaunchKernelGGL((k_subsweep_fallback<NSLOT, NMC>), dim3(64), dim3(kWave * kSubWaves), lds_full, st,
                            g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0);
     }
