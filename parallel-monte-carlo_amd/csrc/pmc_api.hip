@@ -96,6 +96,8 @@ DevGeom make_geom(const pmc_params& p) {
     g.rc2 = pmc_cutoff_r2(p.w);
     g.rc2f = pmc_filter_r2(g.rc2);
     g.r2min = PMC_R2_MIN;
+    g.div_ncx = make_udiv_magic((uint32_t)(p.cps_x / 2));
+    g.div_ncy = make_udiv_magic((uint32_t)(p.cps_y / 2));
     g.k0 = (uint32_t)p.seed;
     g.k1 = (uint32_t)(p.seed >> 32);
     return g;

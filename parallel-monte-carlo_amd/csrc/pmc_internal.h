@@ -17,13 +17,29 @@ __host__ __device__ constexpr int lds_floats_per_wave(int stride) { return 5 * s
 constexpr int kMainStride = 240;    // main launch: lds_floats_per_wave(240) * 4 B = 5056 B <= 5 KiB
 constexpr int kStatCounters = 4;   // de_fixed, accepted, trials, evaluated
 
+// Unsigned division by an invariant d: n / d = (hi + ((n - hi) >> sh1)) >> sh2, hi = umulhi(n, mul)
+// (Granlund & Montgomery 1994, round-up variant; exact for every 32-bit n).
+struct UDivMagic {
+    uint32_t mul, sh1, sh2;
+};
+inline UDivMagic make_udiv_magic(uint32_t d) {
+    uint32_t l = 0;
+    while (l < 32 && (1ull << l) < d) ++l;                 // ceil(log2 d)
+    UDivMagic m;
+    m.mul = (uint32_t)((((1ull << l) - d) << 32) / d + 1);
+    m.sh1 = l < 1 ? l : 1;
+    m.sh2 = l > 1 ? l - 1 : 0;
+    return m;
+}
+
 // Flattened kernel parameters (passed by value).
 struct DevGeom {
     int cps_x, cps_y, cps_z, nz_local, z0, halo, nmax, n_moves;
     int nslot;                     // power of two >= nmax (lanes per cell in shift/energy)
     float w, beta, sigma, Lx, Ly, Lz, rc2;
     float rc2f;                    // staging filter threshold (pmc_filter_r2)
-    float r2min;                   // PMC_R2_MIN (passed as data so the kernel keeps it in an SGPR)
+    float r2min;
+    UDivMagic div_ncx, div_ncy;    // division by cps_x/2 and cps_y/2 (subsweep cell decode)                   // PMC_R2_MIN (passed as data so the kernel keeps it in an SGPR)
     uint32_t k0, k1;
 };
 

@@ -16,6 +16,7 @@
 // Build with -ffp-contract=off: every float/double op must stay a single IEEE op (the oracle,
 // compiled by gcc with the same flag, reproduces the results bit for bit).
 #include <cstdlib>
+#include <type_traits>
 
 #include "pmc_internal.h"
 #include "../../include/pmc_detmath.h"
@@ -58,6 +59,51 @@ __device__ __forceinline__ int mbcnt64_add(unsigned long long m, int add) {
 }
 __device__ __forceinline__ int mbcnt64(unsigned long long m) { return mbcnt64_add(m, 0); }
 
+__device__ __forceinline__ uint32_t bit_of(uint32_t m, int lane) { return (m >> (lane & 31)) & 1u; }
+
+// Stencil lane masks: lane k = 9*hx + 3*hy + hz < 27; Neg[a] has the lanes whose offset along
+// axis a is -1 (h == 1), Pos[a] those with +1 (h == 2).
+constexpr uint32_t stencil_mask(int axis, int h) {
+    uint32_t m = 0;
+    for (int l = 0; l < 27; ++l) {
+        const int hh = axis == 0 ? l / 9 : (axis == 1 ? (l / 3) % 3 : l % 3);
+        if (hh == h) m |= 1u << l;
+    }
+    return m;
+}
+__device__ constexpr uint32_t kStencilNeg[3] = {stencil_mask(0, 1), stencil_mask(1, 1), stencil_mask(2, 1)};
+__device__ constexpr uint32_t kStencilPos[3] = {stencil_mask(0, 2), stencil_mask(1, 2), stencil_mask(2, 2)};
+
+// lanes of staging pass q whose stencil cell k = 1 + q*CPP + lane/NSLOT is < 27
+template <int NSLOT>
+__device__ constexpr unsigned long long stage_lane_mask(int q) {
+    constexpr int CPP = kWave / NSLOT;
+    unsigned long long m = 0;
+    for (int l = 0; l < kWave; ++l)
+        if (1 + q * CPP + l / NSLOT < 27) m |= 1ull << l;
+    return m;
+}
+
+// Loads from the disk buffer.  OFF32 (buffer < 4 GiB): 32-bit byte offsets -> global_load with an
+// SGPR base and a VGPR offset (no 64-bit address math per load); else 64-bit element addressing.
+template <bool OFF32> struct DiskAddr;
+template <> struct DiskAddr<true> {
+    static constexpr uint32_t kUnit = 4;   // offsets in bytes
+    __device__ static __forceinline__ float ld(const float* b, uint32_t off) {
+        return *(const float*)((const char*)b + (uint64_t)off);
+    }
+};
+template <> struct DiskAddr<false> {
+    static constexpr uint32_t kUnit = 1;   // offsets in floats
+    __device__ static __forceinline__ float ld(const float* b, uint32_t off) { return b[(uint64_t)off]; }
+};
+
+// exact n / d for 32-bit n (Granlund-Montgomery round-up method; magic from make_udiv_magic)
+__device__ __forceinline__ uint32_t udiv_magic(uint32_t n, UDivMagic m) {
+    const uint32_t hi = __umulhi(n, m.mul);
+    return (hi + ((n - hi) >> m.sh1)) >> m.sh2;
+}
+
 // storage index of local cell (x, y, zl)
 __device__ __forceinline__ int64_t sidx(const DevGeom& g, int x, int y, int zl) {
     return (int64_t)x + (int64_t)g.cps_x * ((int64_t)y + (int64_t)g.cps_y * (int64_t)(zl + g.halo));
@@ -88,7 +134,7 @@ __device__ __forceinline__ int64_t sidx(const DevGeom& g, int x, int y, int zl) 
 // ------------------------------------------------------------------------------------------
 // Returns false (and leaves the cell untouched) when the cell's staged partners do not fit the
 // LDS capacity `cap`; the caller queues it for the full-capacity fallback launch.
-template <int NSLOT, int NMC, int STRIDE>
+template <int NSLOT, int NMC, int STRIDE, bool OFF32>
 __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restrict__ disk,
                                               const int16_t* __restrict__ ncnt, int ox, int oy, int oz,
                                               uint32_t sweep, unsigned long long* __restrict__ stats,
@@ -101,52 +147,57 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     const int stride = STRIDE > 0 ? STRIDE : stride_rt;   // compile-time -> LDS offset immediates
     float* py_ = px_ + stride;
     float* pz_ = py_ + stride;
-    const int ncx = g.cps_x >> 1, ncy = g.cps_y >> 1;
-    const int ta = wave_uniform(t % ncx);
-    const int tb = wave_uniform((t / ncx) % ncy);
-    const int tc = cz0 + wave_uniform(t / (ncx * ncy));   // colour plane (z = 2*tc + oz)
+    // t -> (ta, tb, tc) by host-computed magic division (SALU only)
+    const uint32_t q1 = udiv_magic((uint32_t)t, g.div_ncx);
+    const uint32_t q2 = udiv_magic(q1, g.div_ncy);
+    const int ta = t - (int)q1 * (g.cps_x >> 1);
+    const int tb = (int)q1 - (int)q2 * (g.cps_y >> 1);
+    const int tc = cz0 + (int)q2;                          // colour plane (z = 2*tc + oz)
     const int x = 2 * ta + ox, y = 2 * tb + oy, zl = 2 * tc + oz;
     const int zg0 = g.z0 + zl;
     const int plane = g.cps_x * g.cps_y;
     const uint32_t c = (uint32_t)(x + g.cps_x * y + plane * (zl + g.halo));
     const uint32_t id = (uint32_t)x + (uint32_t)g.cps_x * ((uint32_t)y + (uint32_t)g.cps_y * (uint32_t)zg0);
     const uint32_t k0 = g.k0, k1 = g.k1;
+    const uint32_t row = (uint32_t)(3 * nm);                 // floats per cell
 
-    // ---- 1. stencil table (lane k < 27) and all global loads ------------------------------------
-    uint32_t k_off = c * (uint32_t)(3 * nm);      // element offset of the cell's rows
+    // ---- 1. stencil table (lane k < 27; lanes >= 27 compute some in-range cell, unused) -------
+    // lane k = 9*hx + 3*hy + hz, h = 0, 1, 2 -> offset 0, -1, +1 (get_neighbors order)
+    const int dx = (int)bit_of(kStencilPos[0], lane) - (int)bit_of(kStencilNeg[0], lane);
+    const int dy = (int)bit_of(kStencilPos[1], lane) - (int)bit_of(kStencilNeg[1], lane);
+    const int dz = (int)bit_of(kStencilPos[2], lane) - (int)bit_of(kStencilNeg[2], lane);
     float k_sx = 0.0f, k_sy = 0.0f, k_sz = 0.0f;
-    if (lane < 27) {
-        const int hx = lane / 9, hy = (lane / 3) % 3, hz = lane % 3;   // {0,-1,+1} order
-        int nx = x + (hx == 0 ? 0 : (hx == 1 ? -1 : 1));
-        int ny = y + (hy == 0 ? 0 : (hy == 1 ? -1 : 1));
-        const int dz = hz == 0 ? 0 : (hz == 1 ? -1 : 1);
-        if (nx < 0) { nx += g.cps_x; k_sx = -g.Lx; } else if (nx >= g.cps_x) { nx -= g.cps_x; k_sx = g.Lx; }
-        if (ny < 0) { ny += g.cps_y; k_sy = -g.Ly; } else if (ny >= g.cps_y) { ny -= g.cps_y; k_sy = g.Ly; }
-        const int zgn = zg0 + dz;
-        if (zgn < 0) k_sz = -g.Lz; else if (zgn >= g.cps_z) k_sz = g.Lz;
-        int nzl = zl + dz;
-        if (!g.halo) nzl = nzl < 0 ? nzl + g.cps_z : (nzl >= g.cps_z ? nzl - g.cps_z : nzl);
-        k_off = (uint32_t)(nx + g.cps_x * ny + plane * (nzl + g.halo)) * (uint32_t)(3 * nm);
-    }
-    const int k_cnt = ncnt[k_off / (uint32_t)(3 * nm)];
+    int nx = x + dx, ny = y + dy;
+    if (nx < 0) { nx += g.cps_x; k_sx = -g.Lx; } else if (nx >= g.cps_x) { nx -= g.cps_x; k_sx = g.Lx; }
+    if (ny < 0) { ny += g.cps_y; k_sy = -g.Ly; } else if (ny >= g.cps_y) { ny -= g.cps_y; k_sy = g.Ly; }
+    const int zgn = zg0 + dz;
+    if (zgn < 0) k_sz = -g.Lz; else if (zgn >= g.cps_z) k_sz = g.Lz;
+    int nzl = zl + dz;
+    if (!g.halo) nzl = nzl < 0 ? nzl + g.cps_z : (nzl >= g.cps_z ? nzl - g.cps_z : nzl);
+    const uint32_t kc = (uint32_t)(nx + g.cps_x * ny + plane * (nzl + g.halo));
+    const int k_cnt = ncnt[kc];
+    const uint32_t k_off = kc * row * DiskAddr<OFF32>::kUnit;   // bytes (OFF32) or floats
     const int p = lane & (NSLOT - 1);
     const int kk = lane / NSLOT;
     const int pp = p < nm ? p : 0;
+    const uint32_t pp_off = (uint32_t)pp * DiskAddr<OFF32>::kUnit;
+    const uint32_t nm_off = (uint32_t)nm * DiskAddr<OFF32>::kUnit;
     float vx[NP], vy[NP], vz[NP];
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
         const int k = 1 + q * CPP + kk;
-        const uint32_t off = (uint32_t)__shfl((int)k_off, k < 27 ? k : 26) + (uint32_t)pp;
-        vx[q] = disk[off];
-        vy[q] = disk[off + nm];
-        vz[q] = disk[off + 2 * nm];
+        const uint32_t off = (uint32_t)__shfl((int)k_off, k < 27 ? k : 26) + pp_off;
+        vx[q] = DiskAddr<OFF32>::ld(disk, off);
+        vy[q] = DiskAddr<OFF32>::ld(disk, off + nm_off);
+        vz[q] = DiskAddr<OFF32>::ld(disk, off + 2 * nm_off);
     }
     float ownx, owny, ownz;
     {
-        const uint32_t off = c * (uint32_t)(3 * nm) + (uint32_t)(lane < nm ? lane : 0);
-        ownx = disk[off];
-        owny = disk[off + nm];
-        ownz = disk[off + 2 * nm];
+        const float* own = disk + (uint64_t)c * row;           // wave-uniform base
+        const int l = lane < nm ? lane : 0;
+        ownx = own[l];
+        owny = own[nm + l];
+        ownz = own[2 * nm + l];
     }
 
     // ---- 2. random numbers for the first 16 moves + the shuffle (overlaps the loads) ------------
@@ -197,25 +248,43 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     float blo[3], bhi[3];
     pmc_cell_box(x, y, zg0, g.w, g.Lx, g.Ly, g.Lz, blo, bhi);
     int S_nb = 0;
+    // periodic images only matter for cells on the box faces (apply_PBC, subsweep.h:139-151):
+    // interior waves skip the image adds (an add of +0 changes nothing downstream -- staged
+    // coordinates only enter differences that are squared)
+    const bool edge = x == 0 || x == g.cps_x - 1 || y == 0 || y == g.cps_y - 1 || zg0 == 0 ||
+                      zg0 == g.cps_z - 1;
+    auto stage = [&](auto with_image) {
 #pragma unroll
-    for (int q = 0; q < NP; ++q) {
-        const int k = 1 + q * CPP + kk;
-        const int ks = k < 27 ? k : 26;
-        const int cnt = __shfl(k_cnt, ks);
-        // periodic image of stencil cell k (apply_PBC, subsweep.h:139-151, per staged cell)
-        const float ux = vx[q] + __shfl(k_sx, ks);
-        const float uy = vy[q] + __shfl(k_sy, ks);
-        const float uz = vz[q] + __shfl(k_sz, ks);
-        const bool keep = (k < 27) && (p < cnt) && (pmc_box_d2(ux, uy, uz, blo, bhi) <= g.rc2f);
-        const unsigned long long mk = __ballot(keep);
-        const int dst = S_nb + mbcnt64(mk);
-        if (keep && dst < cap_nb) {
-            px_[dst] = ux;
-            py_[dst] = uy;
-            pz_[dst] = uz;
+        for (int q = 0; q < NP; ++q) {
+            const int k = 1 + q * CPP + kk;
+            const int ks = k < 27 ? k : 26;
+            const int cnt = __shfl(k_cnt, ks);
+            float ux = vx[q], uy = vy[q], uz = vz[q];
+            if constexpr (decltype(with_image)::value) {
+                ux = ux + __shfl(k_sx, ks);
+                uy = uy + __shfl(k_sy, ks);
+                uz = uz + __shfl(k_sz, ks);
+            }
+            // lanes of stencil cells k < 27 (compile-time per pass), slot < count, box filter
+            const unsigned long long live = stage_lane_mask<NSLOT>(q);
+            const unsigned long long mk = __builtin_amdgcn_ballot_w64(pmc_box_d2(ux, uy, uz, blo, bhi) <= g.rc2f) &
+                                          __builtin_amdgcn_ballot_w64(p < cnt) & live;
+            const int nk = wave_uniform(__popcll(mk));
+            if (S_nb + nk <= cap_nb) {            // otherwise the cell goes to the fallback
+                float* hx = px_ + S_nb;
+                if (__builtin_amdgcn_inverse_ballot_w64(mk)) {
+                    const int dst = mbcnt64(mk);
+                    hx[dst] = ux;
+                    hx[stride + dst] = uy;
+                    hx[2 * stride + dst] = uz;
+                }
+            }
+            S_nb += nk;
         }
-        S_nb += __popcll(mk);
-    }
+    };
+    if (edge) stage(std::true_type{});
+    else stage(std::false_type{});
+    S_nb = wave_uniform(S_nb);   // keep it scalar past the divergent stores (structurizer joins)
     if (S_nb > cap_nb) return false;                            // -> full-capacity fallback
     {
         const float sxo = as_f(__shfl(as_i(ownx), perm));
@@ -334,7 +403,7 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
 // Main launch: one wave per cell of the colour; LDS layout stride kMainStride, capacity `cap`
 // (<= kMainStride) partners per wave (sized for the occupancy; a cell whose filtered stencil
 // exceeds it is queued in ovf for the fallback).
-template <int NSLOT, int NMC>
+template <int NSLOT, int NMC, bool OFF32>
 __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep(DevGeom g, float* __restrict__ disk,
                                                                   const int16_t* __restrict__ ncnt,
                                                                   int ox, int oy, int oz, uint32_t sweep,
@@ -350,7 +419,7 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep(DevGeom g, float
     const int total = (g.cps_x >> 1) * (g.cps_y >> 1) * ncz;
     const int t = (int)b * kSubWaves + wv;
     if (t >= total) return;
-    if (!subsweep_wave<NSLOT, NMC, kMainStride>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, kMainStride, cap,
+    if (!subsweep_wave<NSLOT, NMC, kMainStride, OFF32>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, kMainStride, cap,
                                                 t, cz0)) {
         if ((threadIdx.x & (kWave - 1)) == 0) ovf[1 + atomicAdd(&ovf[0], 1)] = t;
     }
@@ -358,7 +427,7 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep(DevGeom g, float
 
 // Fallback launch: full capacity (27*nmax partners per wave), a fixed grid striding over the
 // queued cells.  Cells of one colour are independent, so the order does not matter.
-template <int NSLOT, int NMC>
+template <int NSLOT, int NMC, bool OFF32>
 __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_fallback(DevGeom g, float* __restrict__ disk,
                                                                            const int16_t* __restrict__ ncnt,
                                                                            int ox, int oy, int oz, uint32_t sweep,
@@ -371,7 +440,7 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_fallback(DevGeom
     const int count = __builtin_amdgcn_readfirstlane(ovf[0]);
     for (int e = (int)blockIdx.x * kSubWaves + wv; e < count; e += (int)gridDim.x * kSubWaves) {
         const int t = __builtin_amdgcn_readfirstlane(ovf[1 + e]);
-        (void)subsweep_wave<NSLOT, NMC, 27 * NMC>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, full, full, t,
+        (void)subsweep_wave<NSLOT, NMC, 27 * NMC, OFF32>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, full, full, t,
                                                   cz0);
     }
 }
@@ -629,7 +698,7 @@ int subsweep_capacity(const DevGeom& g) {
     return kMainStride < full ? kMainStride : full;
 }
 
-template <int NSLOT, int NMC>
+template <int NSLOT, int NMC, bool OFF32>
 static void launch_subsweep_t(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
                               uint32_t sweep, unsigned long long* stats, int* ovf, int cz0, int ncz,
                               hipStream_t st) {
@@ -638,13 +707,25 @@ static void launch_subsweep_t(const DevGeom& g, float* disk, const int16_t* n, i
     const int cap = subsweep_capacity(g);
     const int full = 27 * g.nmax;
     const size_t lds = sizeof(float) * (size_t)lds_floats_per_wave(kMainStride) * kSubWaves;
-    hipLaunchKernelGGL((k_subsweep<NSLOT, NMC>), dim3((unsigned)blocks), dim3(kWave * kSubWaves), lds, st, g,
+    hipLaunchKernelGGL((k_subsweep<NSLOT, NMC, OFF32>), dim3((unsigned)blocks), dim3(kWave * kSubWaves), lds, st, g,
                        disk, n, ox, oy, oz, sweep, stats, cap, ovf, cz0, ncz);
     if (cap < full) {
         const size_t lds_full = sizeof(float) * (size_t)lds_floats_per_wave(full) * kSubWaves;
-        hipLaunchKernelGGL((k_subsweep_fallback<NSLOT, NMC>), dim3(64), dim3(kWave * kSubWaves), lds_full, st,
+        hipLaunchKernelGGL((k_subsweep_fallback<NSLOT, NMC, OFF32>), dim3(64), dim3(kWave * kSubWaves), lds_full, st,
                            g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0);
     }
+}
+
+template <bool OFF32>
+static void launch_subsweep_n(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
+                              uint32_t sweep, unsigned long long* stats, int* ovf, int cz0, int ncz,
+                              hipStream_t st) {
+    if (g.nmax == 16) launch_subsweep_t<16, 16, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st);
+    else if (g.nmax == 32) launch_subsweep_t<32, 32, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st);
+    else if (g.nslot == 8) launch_subsweep_t<8, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st);
+    else if (g.nslot == 16) launch_subsweep_t<16, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st);
+    else if (g.nslot == 32) launch_subsweep_t<32, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st);
+    else launch_subsweep_t<64, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st);
 }
 
 hipError_t launch_subsweep(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
@@ -659,12 +740,12 @@ hipError_t launch_subsweep(const DevGeom& g, float* disk, const int16_t* n, int 
     const int ncz = cz1 - cz0;
     hipError_t e = hipMemsetAsync(ovf, 0, sizeof(int), st);
     if (e != hipSuccess) return e;
-    if (g.nmax == 16) launch_subsweep_t<16, 16>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st);
-    else if (g.nmax == 32) launch_subsweep_t<32, 32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st);
-    else if (g.nslot == 8) launch_subsweep_t<8, 0>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st);
-    else if (g.nslot == 16) launch_subsweep_t<16, 0>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st);
-    else if (g.nslot == 32) launch_subsweep_t<32, 0>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st);
-    else launch_subsweep_t<64, 0>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st);
+    // 32-bit byte offsets when the disk buffer is below 4 GiB (every single-GPU 256^3 config)
+    // (test hook: PMC_FORCE_ADDR64 takes the 64-bit path for any size)
+    static const bool force64 = std::getenv("PMC_FORCE_ADDR64") != nullptr;
+    const int64_t bytes = (int64_t)g.cps_x * g.cps_y * (g.nz_local + 2 * g.halo) * 3 * g.nmax * 4;
+    if (!force64 && bytes < ((int64_t)1 << 32)) launch_subsweep_n<true>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st);
+    else launch_subsweep_n<false>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st);
     return hipGetLastError();
 }
 

@@ -172,10 +172,14 @@ def test_single_colour_parity_128(pmc, oracle):
     assert abs(r["e_initial"] + r["de_fixed"] / 2**32 - r["e_final"]) < 1e-4 * abs(r["e_final"])
 
 
-def test_fallback_capacity_path(oracle):
-    """Cells whose filtered stencil exceeds the main launch's LDS capacity are processed by the
-    full-capacity fallback launch; forcing a tiny capacity sends (almost) every cell there and the
-    result must still be bit-identical.  Runs in a subprocess (the capacity is read once)."""
+@pytest.mark.parametrize("env,nmax", [({"PMC_SUBSWEEP_CAP": "64"}, 32),
+                                      ({"PMC_FORCE_ADDR64": "1"}, 16),
+                                      ({"PMC_FORCE_ADDR64": "1", "PMC_SUBSWEEP_CAP": "64"}, 16)])
+def test_fallback_and_addr64_paths(oracle, env, nmax):
+    """Test hooks for launch variants the default configs never take, each bit-identical to the
+    oracle: PMC_SUBSWEEP_CAP forces a tiny LDS capacity, so (almost) every cell goes to the
+    full-capacity fallback launch; PMC_FORCE_ADDR64 forces the 64-bit disk addressing used for
+    buffers of 4 GiB and more.  Runs in a subprocess (the hooks are read once)."""
     import os
     import subprocess
     import sys
@@ -183,22 +187,23 @@ def test_fallback_capacity_path(oracle):
 import sys, numpy as np
 sys.path[:0] = [sys.argv[1], sys.argv[2]]
 import pmc_amd, pmc_oracle
-ctx = pmc_amd.PmcContext(8, nmax=32)
+nmax = int(sys.argv[3])
+ctx = pmc_amd.PmcContext(8, nmax=nmax)
 ctx.init_lattice(4000)
 r = ctx.start(0, 3)
 disk, n = ctx.copy_out()
-st = pmc_oracle.OracleState(pmc_oracle.make_params(cps=8, nmax=32))
+st = pmc_oracle.OracleState(pmc_oracle.make_params(cps=8, nmax=nmax))
 st.init_lattice(4000)
 st.run(0, 3)
 assert np.array_equal(n, st.n)
-assert pmc_oracle.valid_slots_equal(disk, n, st.disk, st.n, 32)
+assert pmc_oracle.valid_slots_equal(disk, n, st.disk, st.n, nmax)
 assert r["accepted"] == st.stats.accepted and r["trials"] == st.stats.trials
 print("ok", r["accepted"])
 '''
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, PMC_SUBSWEEP_CAP="64")
     out = subprocess.run([sys.executable, "-c", code, os.path.join(repo, "parallel-monte-carlo_amd"),
-                          os.path.join(repo, "oracle")], env=env, capture_output=True, text=True, timeout=300)
+                          os.path.join(repo, "oracle"), str(nmax)], env=dict(os.environ, **env),
+                         capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-2000:]
     assert out.stdout.startswith("ok")
 
