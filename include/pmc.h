@@ -82,6 +82,8 @@ int pmc_create(const pmc_params* params, pmc_ctx** out);
 void pmc_destroy(pmc_ctx* ctx);
 /* Enqueue all further work on `stream` (a hipStream_t; NULL = the null stream). */
 int pmc_set_stream(pmc_ctx* ctx, void* stream);
+/* The stream the context enqueues on (a hipStream_t), for ordering caller work against it. */
+int pmc_get_stream(pmc_ctx* ctx, void** stream);
 /* Use caller-owned device buffers as the context state instead of its own (e.g. torch
  * tensors for RCCL halo exchange).  Each disk buffer holds storage_cells*3*nmax floats, each
  * n buffer storage_cells int16; buffer 0 is the current state. */

@@ -223,6 +223,12 @@ int pmc_set_stream(pmc_ctx* c, void* stream) {
     return PMC_OK;
 }
 
+int pmc_get_stream(pmc_ctx* c, void** stream) {
+    if (!c || !stream) return fail(PMC_ERR_ARG, "null argument");
+    *stream = (void*)c->stream;
+    return PMC_OK;
+}
+
 int pmc_attach_state(pmc_ctx* c, float* disk0, int16_t* n0, float* disk1, int16_t* n1) {
     if (!c || !disk0 || !n0 || !disk1 || !n1) return fail(PMC_ERR_ARG, "null argument");
     PMC_HIP(hipStreamSynchronize(c->stream));

@@ -449,83 +449,94 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_fallback(DevGeom
 // shiftCells: NSLOT lanes per cell, ballot compaction (shiftCells.h:28-144; float s of the fixed
 // copy CUDA-Parallel-MC/CUDA-Parallel-MC/shiftCells.h:23-112).  Double-buffered.
 // ------------------------------------------------------------------------------------------
-template <int NSLOT>
+template <int NSLOT, int U>
 __global__ __launch_bounds__(256) void k_shift(DevGeom g, const float* __restrict__ din,
                                                const int16_t* __restrict__ nin, float* __restrict__ dout,
                                                int16_t* __restrict__ nout, int f, float d,
                                                uint32_t* __restrict__ flags) {
-    // grid: (ceil(cps_x / CPB), cps_y, nz_local); NSLOT lanes per cell, CPB cells per block along x
+    // grid: (ceil(cps_x / (CPB*U)), cps_y, nz_local); NSLOT lanes per cell, CPB cells per block
+    // along x per unrolled step j, U steps whose loads are all issued before any use (U times
+    // the bytes in flight per wave: the kernel is latency-bound at one cell per lane group)
     constexpr int CPB = 256 / NSLOT;
     const int lane = threadIdx.x & (kWave - 1);
     const int p = threadIdx.x & (NSLOT - 1);
-    const int x = (int)blockIdx.x * CPB + (int)(threadIdx.x / NSLOT);
     const int y = (int)blockIdx.y, zl = (int)blockIdx.z;
-    const bool live = x < g.cps_x;
     const int nm = g.nmax;
     const float w = g.w;
-
     const int cps_f = f == 0 ? g.cps_x : (f == 1 ? g.cps_y : g.cps_z);
     const float Lf = f == 0 ? g.Lx : (f == 1 ? g.Ly : g.Lz);
     const int dir = (d <= 0) ? -1 : 1;                     // shiftCells.h:46-53
     const float s = w * (float)dir;
-    const int xx = live ? x : 0;
-    const int cidf = f == 0 ? xx : (f == 1 ? y : g.z0 + zl);
-    const float offset = (float)cidf * w - Lf / 2.0f;     // :55
-    int nbg = cidf + dir;
-    if (nbg < 0) nbg = cps_f - 1; else if (nbg >= cps_f) nbg = 0;
-    int nx = xx, ny = y, nz = zl;
-    if (f == 0) nx = nbg; else if (f == 1) ny = nbg; else nz = g.halo ? zl + dir : nbg;
-    const float offset_nb = (float)nbg * w - Lf / 2.0f;
     const uint32_t plane = (uint32_t)g.cps_x * (uint32_t)g.cps_y;
-    const uint32_t c = (uint32_t)xx + (uint32_t)g.cps_x * (uint32_t)y + plane * (uint32_t)(zl + g.halo);
-    const uint32_t cnb = (uint32_t)nx + (uint32_t)g.cps_x * (uint32_t)ny + plane * (uint32_t)(nz + g.halo);
-
-    // one round trip: both counts and all six rows (a 64 B row sits inside one 128 B line)
-    const int ncur = live ? nin[c] : 0;
-    const int nnb = live ? nin[cnb] : 0;
     const int pp = p < nm ? p : 0;
-    const uint32_t oc = c * (uint32_t)(3 * nm) + (uint32_t)pp, on = cnb * (uint32_t)(3 * nm) + (uint32_t)pp;
-    float own[3], nbv[3];
-#pragma unroll
-    for (int dim = 0; dim < 3; ++dim) {
-        own[dim] = din[oc + (uint32_t)(dim * nm)];
-        nbv[dim] = din[on + (uint32_t)(dim * nm)];
-    }
-    const float xf = f == 0 ? own[0] : (f == 1 ? own[1] : own[2]);
-    const float xfn = f == 0 ? nbv[0] : (f == 1 ? nbv[1] : nbv[2]);
-    const float D = (xf - offset) - d;                    // shortDisk - d
-    const float Dn = (xfn - offset_nb) - d;
-    const bool keep = (p < ncur) && (D > 0 && D <= w);
-    const bool take = (p < nnb) && !(Dn > 0 && Dn <= w);
-    const unsigned long long bk = __ballot(keep);
-    const unsigned long long bt = __ballot(take);
     const int gsh = lane & ~(NSLOT - 1);
     const unsigned long long gmask = NSLOT == 64 ? ~0ull : ((1ull << NSLOT) - 1ull);
-    const unsigned long long km = (bk >> gsh) & gmask;
-    const unsigned long long tm = (bt >> gsh) & gmask;
     const unsigned long long below = (1ull << p) - 1ull;
-    const int nk = __popcll(km);
-    const int nnew = nk + __popcll(tm);
-    const uint32_t ob = c * (uint32_t)(3 * nm);
-    if (keep) {
-        const int dst = __popcll(km & below);
-        if (dst < nm) {
+
+    bool live[U];
+    uint32_t c[U];
+    int ncur[U], nnb[U];
+    float offset[U], offset_nb[U], own[U][3], nbv[U][3];
 #pragma unroll
-            for (int dim = 0; dim < 3; ++dim)
-                dout[ob + (uint32_t)(dim * nm + dst)] = (dim == f) ? D + offset : own[dim];
+    for (int j = 0; j < U; ++j) {
+        const int x = ((int)blockIdx.x * U + j) * CPB + (int)(threadIdx.x / NSLOT);
+        live[j] = x < g.cps_x;
+        const int xx = live[j] ? x : 0;
+        const int cidf = f == 0 ? xx : (f == 1 ? y : g.z0 + zl);
+        offset[j] = (float)cidf * w - Lf / 2.0f;           // :55
+        int nbg = cidf + dir;
+        if (nbg < 0) nbg = cps_f - 1; else if (nbg >= cps_f) nbg = 0;
+        int nx = xx, ny = y, nz = zl;
+        if (f == 0) nx = nbg; else if (f == 1) ny = nbg; else nz = g.halo ? zl + dir : nbg;
+        offset_nb[j] = (float)nbg * w - Lf / 2.0f;
+        c[j] = (uint32_t)xx + (uint32_t)g.cps_x * (uint32_t)y + plane * (uint32_t)(zl + g.halo);
+        const uint32_t cnb = (uint32_t)nx + (uint32_t)g.cps_x * (uint32_t)ny + plane * (uint32_t)(nz + g.halo);
+        // one round trip: both counts and all six rows (a 64 B row sits inside one 128 B line)
+        // unconditional loads (c, cnb are valid cells for dead lanes too: no branch, no wait)
+        const int nc0 = nin[c[j]], nn0 = nin[cnb];
+        ncur[j] = live[j] ? nc0 : 0;
+        nnb[j] = live[j] ? nn0 : 0;
+        const uint64_t oc = (uint64_t)c[j] * (uint64_t)(3 * nm) + (uint64_t)pp;
+        const uint64_t on = (uint64_t)cnb * (uint64_t)(3 * nm) + (uint64_t)pp;
+#pragma unroll
+        for (int dim = 0; dim < 3; ++dim) {
+            own[j][dim] = din[oc + (uint64_t)(dim * nm)];
+            nbv[j][dim] = din[on + (uint64_t)(dim * nm)];
         }
     }
-    if (take) {
-        const int dst = nk + __popcll(tm & below);
-        if (dst < nm) {
 #pragma unroll
-            for (int dim = 0; dim < 3; ++dim)
-                dout[ob + (uint32_t)(dim * nm + dst)] = (dim == f) ? ((Dn + offset) + s) : nbv[dim];
+    for (int j = 0; j < U; ++j) {
+        const float xf = f == 0 ? own[j][0] : (f == 1 ? own[j][1] : own[j][2]);
+        const float xfn = f == 0 ? nbv[j][0] : (f == 1 ? nbv[j][1] : nbv[j][2]);
+        const float D = (xf - offset[j]) - d;               // shortDisk - d
+        const float Dn = (xfn - offset_nb[j]) - d;
+        const bool keep = (p < ncur[j]) && (D > 0 && D <= w);
+        const bool take = (p < nnb[j]) && !(Dn > 0 && Dn <= w);
+        const unsigned long long km = (__ballot(keep) >> gsh) & gmask;
+        const unsigned long long tm = (__ballot(take) >> gsh) & gmask;
+        const int nk = __popcll(km);
+        const int nnew = nk + __popcll(tm);
+        const uint64_t ob = (uint64_t)c[j] * (uint64_t)(3 * nm);
+        if (keep) {
+            const int dst = __popcll(km & below);
+            if (dst < nm) {
+#pragma unroll
+                for (int dim = 0; dim < 3; ++dim)
+                    dout[ob + (uint64_t)(dim * nm + dst)] = (dim == f) ? D + offset[j] : own[j][dim];
+            }
         }
-    }
-    if (live && p == 0) {
-        nout[c] = (int16_t)(nnew > nm ? nm : nnew);
-        if (nnew > nm) atomicOr(flags, 1u);
+        if (take) {
+            const int dst = nk + __popcll(tm & below);
+            if (dst < nm) {
+#pragma unroll
+                for (int dim = 0; dim < 3; ++dim)
+                    dout[ob + (uint64_t)(dim * nm + dst)] = (dim == f) ? ((Dn + offset_nb[j]) + s) : nbv[j][dim];
+            }
+        }
+        if (live[j] && p == 0) {
+            nout[c[j]] = (int16_t)(nnew > nm ? nm : nnew);
+            if (nnew > nm) atomicOr(flags, 1u);
+        }
     }
 }
 
@@ -751,13 +762,14 @@ hipError_t launch_subsweep(const DevGeom& g, float* disk, const int16_t* n, int 
 
 hipError_t launch_shift(const DevGeom& g, const float* din, const int16_t* nin, float* dout,
                         int16_t* nout, int f, float d, uint32_t* flags, hipStream_t st) {
+    constexpr int U = 4;   // cells per lane group, loads hoisted
     const int cpb = 256 / g.nslot;
-    dim3 grid((unsigned)((g.cps_x + cpb - 1) / cpb), (unsigned)g.cps_y, (unsigned)g.nz_local), block(256);
+    dim3 grid((unsigned)((g.cps_x + cpb * U - 1) / (cpb * U)), (unsigned)g.cps_y, (unsigned)g.nz_local), block(256);
     switch (g.nslot) {
-        case 8: hipLaunchKernelGGL(k_shift<8>, grid, block, 0, st, g, din, nin, dout, nout, f, d, flags); break;
-        case 16: hipLaunchKernelGGL(k_shift<16>, grid, block, 0, st, g, din, nin, dout, nout, f, d, flags); break;
-        case 32: hipLaunchKernelGGL(k_shift<32>, grid, block, 0, st, g, din, nin, dout, nout, f, d, flags); break;
-        default: hipLaunchKernelGGL(k_shift<64>, grid, block, 0, st, g, din, nin, dout, nout, f, d, flags); break;
+        case 8: hipLaunchKernelGGL((k_shift<8, U>), grid, block, 0, st, g, din, nin, dout, nout, f, d, flags); break;
+        case 16: hipLaunchKernelGGL((k_shift<16, U>), grid, block, 0, st, g, din, nin, dout, nout, f, d, flags); break;
+        case 32: hipLaunchKernelGGL((k_shift<32, U>), grid, block, 0, st, g, din, nin, dout, nout, f, d, flags); break;
+        default: hipLaunchKernelGGL((k_shift<64, U>), grid, block, 0, st, g, din, nin, dout, nout, f, d, flags); break;
     }
     return hipGetLastError();
 }

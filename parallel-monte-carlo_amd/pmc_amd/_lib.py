@@ -92,6 +92,7 @@ def lib():
         _sig(L, "pmc_create", i32, P, C.POINTER(_vp))
         _sig(L, "pmc_destroy", None, _vp)
         _sig(L, "pmc_set_stream", i32, _vp, _vp)
+        _sig(L, "pmc_get_stream", i32, _vp, C.POINTER(_vp))
         _sig(L, "pmc_attach_state", i32, _vp, _vp, _vp, _vp, _vp)
         _sig(L, "pmc_state", i32, _vp, C.POINTER(_vp), C.POINTER(_vp))
         _sig(L, "pmc_storage_cells", i64, _vp)

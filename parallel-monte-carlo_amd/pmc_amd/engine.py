@@ -8,11 +8,14 @@ Reference entry points (qingye3/parallel-monte-carlo):
   main (the `start` program)                       start.cu:169  -> PmcContext.start
 
 Buffers passed to the reference-kernel methods are device pointers (ints) or torch CUDA tensors
-in the reference layout; the driver methods act on the context-owned state.  Every call goes to
-the HIP library -- there is no CPU path.
+in the reference layout; the driver methods act on the context-owned state.  With torch tensors
+the launch is ordered after torch's current stream and torch's current stream after the launch
+(stream waits, no host sync), so tensors can be produced and consumed with ordinary torch ops.
+Every call goes to the HIP library -- there is no CPU path.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 from typing import Optional
 
@@ -84,6 +87,28 @@ class PmcContext:
     def set_stream(self, stream: int):
         check("pmc_set_stream", lib().pmc_set_stream(self._h, C.c_void_p(stream)))
 
+    def stream(self) -> int:
+        st = C.c_void_p()
+        check("pmc_get_stream", lib().pmc_get_stream(self._h, C.byref(st)))
+        return st.value or 0
+
+    @contextlib.contextmanager
+    def _torch_ordered(self, *bufs):
+        """Order a launch on the context stream between torch's current-stream work that
+        produced `bufs` and the torch work that consumes them (device-side stream waits)."""
+        if not any(hasattr(b, "data_ptr") for b in bufs):
+            yield
+            return
+        import torch
+        ours = torch.cuda.ExternalStream(self.stream())
+        theirs = torch.cuda.current_stream()
+        if ours.cuda_stream == theirs.cuda_stream:
+            yield
+            return
+        ours.wait_stream(theirs)
+        yield
+        theirs.wait_stream(ours)
+
     def attach_state(self, disk0, n0, disk1, n1):
         check("pmc_attach_state", lib().pmc_attach_state(self._h, _ptr(disk0), _ptr(n0), _ptr(disk1), _ptr(n1)))
 
@@ -94,18 +119,22 @@ class PmcContext:
 
     # ---- reference kernels -------------------------------------------------------------
     def init_r(self, n_atoms: int, r) -> None:
-        check("pmc_init_r", lib().pmc_init_r(self._h, n_atoms, _ptr(r)))
+        with self._torch_ordered(r):
+            check("pmc_init_r", lib().pmc_init_r(self._h, n_atoms, _ptr(r)))
 
     def assign(self, r, n_atoms: int, disk, n) -> None:
-        check("pmc_assign", lib().pmc_assign(self._h, _ptr(r), n_atoms, _ptr(disk), _ptr(n)))
+        with self._torch_ordered(r, disk, n):
+            check("pmc_assign", lib().pmc_assign(self._h, _ptr(r), n_atoms, _ptr(disk), _ptr(n)))
 
     def subsweep_kernel(self, disk, n, offset, sweep: int) -> None:
         off = (C.c_int * 3)(*[int(v) for v in offset])
-        check("pmc_subsweep", lib().pmc_subsweep(self._h, _ptr(disk), _ptr(n), C.byref(off), sweep))
+        with self._torch_ordered(disk, n):
+            check("pmc_subsweep", lib().pmc_subsweep(self._h, _ptr(disk), _ptr(n), C.byref(off), sweep))
 
     def shiftCells(self, disk_in, n_in, disk_out, n_out, f: int, d: float) -> None:  # noqa: N802
-        check("pmc_shift_cells", lib().pmc_shift_cells(self._h, _ptr(disk_in), _ptr(n_in), _ptr(disk_out),
-                                                       _ptr(n_out), f, d))
+        with self._torch_ordered(disk_in, n_in, disk_out, n_out):
+            check("pmc_shift_cells", lib().pmc_shift_cells(self._h, _ptr(disk_in), _ptr(n_in), _ptr(disk_out),
+                                                           _ptr(n_out), f, d))
 
     # ---- driver ------------------------------------------------------------------------
     def init_lattice(self, n_atoms: int) -> None:
