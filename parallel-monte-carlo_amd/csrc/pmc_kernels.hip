@@ -530,7 +530,7 @@ __global__ __launch_bounds__(256) void k_shift(DevGeom g, const float* __restric
             if (dst < nm) {
 #pragma unroll
                 for (int dim = 0; dim < 3; ++dim)
-                    dout[ob + (uint64_t)(dim * nm + dst)] = (dim == f) ? ((Dn + offset_nb[j]) + s) : nbv[j][dim];
+                    dout[ob + (uint64_t)(dim * nm + dst)] = (dim == f) ? ((Dn + offset[j]) + s) : nbv[j][dim];   // own offset (shiftCells.h:100)
             }
         }
         if (live[j] && p == 0) {
@@ -762,7 +762,10 @@ hipError_t launch_subsweep(const DevGeom& g, float* disk, const int16_t* n, int 
 
 hipError_t launch_shift(const DevGeom& g, const float* din, const int16_t* nin, float* dout,
                         int16_t* nout, int f, float d, uint32_t* flags, hipStream_t st) {
-    constexpr int U = 4;   // cells per lane group, loads hoisted
+#ifndef PMC_SHIFT_U
+#define PMC_SHIFT_U 4
+#endif
+    constexpr int U = PMC_SHIFT_U;   // cells per lane group, loads hoisted
     const int cpb = 256 / g.nslot;
     dim3 grid((unsigned)((g.cps_x + cpb * U - 1) / (cpb * U)), (unsigned)g.cps_y, (unsigned)g.nz_local), block(256);
     switch (g.nslot) {
