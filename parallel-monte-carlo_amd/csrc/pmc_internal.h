@@ -12,9 +12,13 @@ namespace pmc {
 constexpr int kWave = 64;          // CDNA wavefront
 constexpr int kSubWaves = 4;       // cells (waves) per subsweep workgroup
 constexpr int kStatSlots = 1024;   // stats accumulator slots per counter (contention spread)
-// subsweep LDS per wave: x, y, z rows of `stride` partner slots + a term list of 2*stride + 64
-__host__ __device__ constexpr int lds_floats_per_wave(int stride) { return 5 * stride + 64; }
-constexpr int kMainStride = 240;    // main launch: lds_floats_per_wave(240) * 4 B = 5056 B <= 5 KiB
+// subsweep LDS per wave for a partner capacity lcap: x, y, z rows of `stride` slots
+// (stride = lcap rounded up to 64 with >= 32 slots of tail: the tail is the discard target of the
+// staging stores and the "far" fill past the last partner), then a term list of 2*lcap + 64.
+__host__ __device__ constexpr int subsweep_stride(int lcap) { return (lcap + 32 + 63) / 64 * 64; }
+__host__ __device__ constexpr int lds_floats_per_wave(int lcap) { return 3 * subsweep_stride(lcap) + 2 * lcap + 64; }
+constexpr int kMainCap = 224;       // main launch: lds_floats_per_wave(224) * 4 B = 5120 B (32 waves/CU)
+static_assert(lds_floats_per_wave(kMainCap) * 4 <= 5120, "main-launch LDS per wave");
 constexpr int kStatCounters = 4;   // de_fixed, accepted, trials, evaluated
 
 // Unsigned division by an invariant d: n / d = (hi + ((n - hi) >> sh1)) >> sh2, hi = umulhi(n, mul)

@@ -129,24 +129,28 @@ __device__ __forceinline__ int64_t sidx(const DevGeom& g, int x, int y, int zl) 
 //      and only those reach the reciprocal -- term t on lane t % 64; one fixed-order
 //      DPP/permlane reduction gives dE; accept in-kernel, wave-uniformly;
 //   5. write back the own cell; one atomic per counter per wave.
-// LDS per wave: x, y, z rows of `stride` partner slots, then the term list (2 * stride + 64
-// floats; the extra 64 let a pass read a full 64-lane block without clamping).
+// LDS per wave (capacity lcap): x, y, z rows of `stride` = subsweep_stride(lcap) slots, then the
+// term list (2 * lcap + 64 floats; the extra 64 are per-lane discard slots and let a pass read a
+// full 64-lane block without clamping).  Row slots past the last partner hold +inf ("far"), as
+// does the moving particle's own slot during its move, so no lane mask is needed in the moves.
 // ------------------------------------------------------------------------------------------
 // Returns false (and leaves the cell untouched) when the cell's staged partners do not fit the
 // LDS capacity `cap`; the caller queues it for the full-capacity fallback launch.
-template <int NSLOT, int NMC, int STRIDE, bool OFF32>
+template <int NSLOT, int NMC, int LCAP, bool OFF32>
 __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restrict__ disk,
                                               const int16_t* __restrict__ ncnt, int ox, int oy, int oz,
                                               uint32_t sweep, unsigned long long* __restrict__ stats,
-                                              float* __restrict__ px_, int stride_rt, int cap, int t,
+                                              float* __restrict__ px_, int lcap_rt, int cap, int t,
                                               int cz0) {
     constexpr int CPP = kWave / NSLOT;            // stencil cells staged per pass
     constexpr int NP = (26 + CPP - 1) / CPP;      // staging passes over the 26 neighbours
     const int lane = threadIdx.x & (kWave - 1);
     const int nm = NMC > 0 ? NMC : g.nmax;        // compile-time for the common nmax
-    const int stride = STRIDE > 0 ? STRIDE : stride_rt;   // compile-time -> LDS offset immediates
+    const int lcap = LCAP > 0 ? LCAP : lcap_rt;            // layout capacity (>= cap)
+    const int stride = subsweep_stride(lcap);              // compile-time -> LDS offset immediates
     float* py_ = px_ + stride;
     float* pz_ = py_ + stride;
+    float* buf = pz_ + stride;                  // term list: signed r2 values
     // t -> (ta, tb, tc) by host-computed magic division (SALU only)
     const uint32_t q1 = udiv_magic((uint32_t)t, g.div_ncx);
     const uint32_t q2 = udiv_magic(q1, g.div_ncy);
@@ -271,13 +275,13 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
                                           __builtin_amdgcn_ballot_w64(p < cnt) & live;
             const int nk = wave_uniform(__popcll(mk));
             if (S_nb + nk <= cap_nb) {            // otherwise the cell goes to the fallback
-                float* hx = px_ + S_nb;
-                if (__builtin_amdgcn_inverse_ballot_w64(mk)) {
-                    const int dst = mbcnt64(mk);
-                    hx[dst] = ux;
-                    hx[stride + dst] = uy;
-                    hx[2 * stride + dst] = uz;
-                }
+                // unconditional stores, discarded lanes into the row tails (>= 32 slots)
+                const int slot = __builtin_amdgcn_inverse_ballot_w64(mk) ? S_nb + mbcnt64(mk)
+                                                                        : stride - 32 + (lane & 31);
+                float* dst = px_ + slot;
+                dst[0] = ux;
+                dst[stride] = uy;
+                dst[2 * stride] = uz;
             }
             S_nb += nk;
         }
@@ -297,6 +301,11 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
         }
     }
     const int K = S_nb + n_own;
+    // slots [K, roundup64(K)) are read by the last 64-lane block of every move: make them "far"
+    // (+inf -> r2 = inf, never listed).  roundup64(K) <= stride; the clamp keeps every lane's
+    // store inside the x row.
+    const float kFar = __builtin_inff();
+    px_[(K + lane) < stride ? K + lane : stride - 1] = kFar;
 
     // cell centre for out_of_bound (subsweep.h:73-88): c*w - L/2 + w/2 in float
     const float hw = g.w / 2.0f;
@@ -305,7 +314,6 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     const float czf = (float)zg0 * g.w - g.Lz / 2.0f + hw;
     const double beta_d = (double)g.beta;
     const float rc2 = g.rc2;
-    float* buf = pz_ + stride;                  // term list: signed r2 values
     // PMC_R2_MIN through an SGPR: v_max_f32 |r2s|, s takes it with the free |.| modifier (a
     // literal operand would force a second max)
     const float r2min = as_f(wave_uniform(as_i(g.r2min)));
@@ -333,32 +341,35 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
                              (__builtin_fabsf(ddz) > hw);
             if (!out) {
                 ++n_ev;
+                px_[si] = kFar;          // exclude the moving particle from its own term list
                 // 4a. term list: per block of 64 partners, the new-position terms within the
                 // cutoff, then the old-position ones (sign bit set), compacted by ballot+mbcnt.
                 // ~80% of staged pairs lie beyond rc for a given position; they are exactly 0
                 // and never reach the reciprocal.
                 int C = 0;   // wave-uniform
-                for (int base = 0; base < K; base += kWave) {
-                    // no clamp: slots in [K, base + 64) are inside this wave's LDS (stride >= 64
-                    // past the x row start, term list padded by 64) and are masked by `ok`
+                // Stores are unconditional: a lane whose term is not listed writes to its own
+                // discard slot 2*lcap + lane past the list (one v_cndmask instead of exec-mask save/restore, which
+                // would cost scalar instructions -- the CU's single scalar unit is the busier
+                // issue port in this loop).
+                auto block = [&](int base) {
+                    // slots >= K and the moving slot hold +inf in x: their r2 is inf, never listed
                     const int k = base + lane;
                     const float xj = px_[k], yj = py_[k], zj = pz_[k];
                     const float r2n = pmc_r2(qx - xj, qy - yj, qz - zj);
                     const float r2o = pmc_r2(xi - xj, yi - yj, zi - zj);
-                    // lanes past K and the moving particle's own slot are masked in SALU
-                    const int rem = K - base;
-                    unsigned long long okm = rem >= kWave ? ~0ull : ((1ull << rem) - 1ull);
-                    const int sr = si - base;
-                    if (sr >= 0 && sr < kWave) okm &= ~(1ull << sr);
-                    const unsigned long long mn = __builtin_amdgcn_ballot_w64(r2n <= rc2) & okm;
-                    const unsigned long long mo = __builtin_amdgcn_ballot_w64(r2o <= rc2) & okm;
+                    const unsigned long long mn = __builtin_amdgcn_ballot_w64(r2n <= rc2);
+                    const unsigned long long mo = __builtin_amdgcn_ballot_w64(r2o <= rc2);
                     const int cn = C + __popcll(mn);
-                    // wave-uniform list heads (SGPR addresses; mbcnt's addend would need a VGPR)
-                    float* hn = buf + C;
-                    float* ho = buf + cn;
-                    if (__builtin_amdgcn_inverse_ballot_w64(mn)) hn[mbcnt64(mn)] = r2n;
-                    if (__builtin_amdgcn_inverse_ballot_w64(mo)) ho[mbcnt64(mo)] = -r2o;
+                    const int dn = __builtin_amdgcn_inverse_ballot_w64(mn) ? C + mbcnt64(mn) : 2 * lcap + lane;
+                    buf[dn] = r2n;
+                    const int dO = __builtin_amdgcn_inverse_ballot_w64(mo) ? cn + mbcnt64(mo) : 2 * lcap + lane;
+                    buf[dO] = -r2o;
                     C = cn + __popcll(mo);
+                };
+                block(0);
+                if (K > kWave) {
+                    block(kWave);
+                    for (int base = 2 * kWave; base < K; base += kWave) block(base);
                 }
                 // 4b. energies of the listed terms: term t on lane t % 64, ascending t
                 float acc = 0.0f;
@@ -372,8 +383,11 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
                 const float dE = wave_sum_fixed_order(4.0f * acc);
                 // dE is wave-uniform (every lane holds the butterfly total): make that explicit
                 const float dEu = as_f(__builtin_amdgcn_readfirstlane(as_i(dE)));
-                if (beta_d * (double)dEu < (double)Tm) {               // accept_move, subsweep.h:209-216
-                    if (lane == 0) { px_[si] = qx; py_[si] = qy; pz_[si] = qz; }
+                const bool acc_mv = beta_d * (double)dEu < (double)Tm;   // accept_move, subsweep.h:209-216
+                px_[si] = acc_mv ? qx : xi;                              // (every lane, same value)
+                if (acc_mv) {
+                    py_[si] = qy;
+                    pz_[si] = qz;
                     ++n_acc;
                     de_cell = de_cell + (double)dEu;
                 }
@@ -400,8 +414,8 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     return true;
 }
 
-// Main launch: one wave per cell of the colour; LDS layout stride kMainStride, capacity `cap`
-// (<= kMainStride) partners per wave (sized for the occupancy; a cell whose filtered stencil
+// Main launch: one wave per cell of the colour; LDS layout for kMainCap partners, capacity `cap`
+// (<= kMainCap) partners per wave (sized for the occupancy; a cell whose filtered stencil
 // exceeds it is queued in ovf for the fallback).
 template <int NSLOT, int NMC, bool OFF32>
 __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep(DevGeom g, float* __restrict__ disk,
@@ -411,7 +425,7 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep(DevGeom g, float
                                                                   int cap, int* __restrict__ ovf, int cz0, int ncz) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform -> SALU math
-    float* px_ = smem + wv * lds_floats_per_wave(kMainStride);
+    float* px_ = smem + wv * lds_floats_per_wave(kMainCap);
     // XCD-aware block order: blocks b and b+8 share an XCD (round-robin dispatch), so give each
     // XCD a contiguous run of cells -> neighbouring stencils share that XCD's L2.  Speed only.
     uint32_t nblk = gridDim.x, b = blockIdx.x;
@@ -419,7 +433,7 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep(DevGeom g, float
     const int total = (g.cps_x >> 1) * (g.cps_y >> 1) * ncz;
     const int t = (int)b * kSubWaves + wv;
     if (t >= total) return;
-    if (!subsweep_wave<NSLOT, NMC, kMainStride, OFF32>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, kMainStride, cap,
+    if (!subsweep_wave<NSLOT, NMC, kMainCap, OFF32>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, kMainCap, cap,
                                                 t, cz0)) {
         if ((threadIdx.x & (kWave - 1)) == 0) ovf[1 + atomicAdd(&ovf[0], 1)] = t;
     }
@@ -697,7 +711,7 @@ __global__ void k_selftest(const uint32_t* __restrict__ words, int count, float*
 int subsweep_capacity(const DevGeom& g) {
     // Partners per wave held in LDS by the main launch.  Sized so a wave needs at most 5 KiB of
     // LDS (-> 32 waves/CU, the hardware limit): 3 floats per partner (x, y, z) + 2 term-list
-    // entries + 64 (kMainStride = 240).  The filtered stencil holds ~98 partners at n = 4.77 per
+    // entries + row tails (kMainCap = 224).  The filtered stencil holds ~98 partners at n = 4.77 per
     // cell; larger ones use the fallback.
     const int full = 27 * g.nmax;
     // test hook: PMC_SUBSWEEP_CAP forces a (small) capacity so the fallback path is exercised
@@ -706,7 +720,7 @@ int subsweep_capacity(const DevGeom& g) {
         return e ? std::atoi(e) : 0;
     }();
     if (forced > 0) return forced < full ? forced : full;
-    return kMainStride < full ? kMainStride : full;
+    return kMainCap < full ? kMainCap : full;
 }
 
 template <int NSLOT, int NMC, bool OFF32>
@@ -717,7 +731,7 @@ static void launch_subsweep_t(const DevGeom& g, float* disk, const int16_t* n, i
     const int64_t blocks = (total + kSubWaves - 1) / kSubWaves;
     const int cap = subsweep_capacity(g);
     const int full = 27 * g.nmax;
-    const size_t lds = sizeof(float) * (size_t)lds_floats_per_wave(kMainStride) * kSubWaves;
+    const size_t lds = sizeof(float) * (size_t)lds_floats_per_wave(kMainCap) * kSubWaves;
     hipLaunchKernelGGL((k_subsweep<NSLOT, NMC, OFF32>), dim3((unsigned)blocks), dim3(kWave * kSubWaves), lds, st, g,
                        disk, n, ox, oy, oz, sweep, stats, cap, ovf, cz0, ncz);
     if (cap < full) {
