@@ -100,6 +100,10 @@ DevGeom make_geom(const pmc_params& p) {
     g.div_ncy = make_udiv_magic((uint32_t)(p.cps_y / 2));
     g.k0 = (uint32_t)p.seed;
     g.k1 = (uint32_t)(p.seed >> 32);
+    for (int r = 0; r < 10; ++r) {
+        g.rk0[r] = g.k0 + (uint32_t)r * PMC_PHILOX_W0;
+        g.rk1[r] = g.k1 + (uint32_t)r * PMC_PHILOX_W1;
+    }
     return g;
 }
 

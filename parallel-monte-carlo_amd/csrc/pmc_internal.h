@@ -10,7 +10,10 @@
 namespace pmc {
 
 constexpr int kWave = 64;          // CDNA wavefront
-constexpr int kSubWaves = 4;       // cells (waves) per subsweep workgroup
+#ifndef PMC_SUBWAVES
+#define PMC_SUBWAVES 4
+#endif
+constexpr int kSubWaves = PMC_SUBWAVES;   // cells (waves) per subsweep workgroup
 constexpr int kStatSlots = 1024;   // stats accumulator slots per counter (contention spread)
 // subsweep LDS per wave for a partner capacity lcap: x, y, z rows of `stride` slots
 // (stride = lcap rounded up to 64 with >= 32 slots of tail: the tail is the discard target of the
@@ -43,7 +46,8 @@ struct DevGeom {
     float w, beta, sigma, Lx, Ly, Lz, rc2;
     float rc2f;                    // staging filter threshold (pmc_filter_r2)
     float r2min;
-    UDivMagic div_ncx, div_ncy;    // division by cps_x/2 and cps_y/2 (subsweep cell decode)                   // PMC_R2_MIN (passed as data so the kernel keeps it in an SGPR)
+    UDivMagic div_ncx, div_ncy;    // division by cps_x/2 and cps_y/2 (subsweep cell decode)
+    uint32_t rk0[10], rk1[10];     // Philox round keys k + r*W (kernel arguments -> SGPRs, no key adds)                   // PMC_R2_MIN (passed as data so the kernel keeps it in an SGPR)
     uint32_t k0, k1;
 };
 

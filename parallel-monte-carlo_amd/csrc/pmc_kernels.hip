@@ -59,6 +59,14 @@ __device__ __forceinline__ int mbcnt64_add(unsigned long long m, int add) {
 }
 __device__ __forceinline__ int mbcnt64(unsigned long long m) { return mbcnt64_add(m, 0); }
 
+// Per-lane select by a wave mask with both arms computed: the empty asm pins `a` in a VGPR, so
+// the compiler emits one v_cndmask instead of sinking a's computation into an exec-masked
+// branch (which costs ~5 scalar instructions of exec bookkeeping per select).
+__device__ __forceinline__ int select_by_mask(unsigned long long m, int a, int b) {
+    asm volatile("" : "+v"(a));
+    return __builtin_amdgcn_inverse_ballot_w64(m) ? a : b;
+}
+
 __device__ __forceinline__ uint32_t bit_of(uint32_t m, int lane) { return (m >> (lane & 31)) & 1u; }
 
 // Stencil lane masks: lane k = 9*hx + 3*hy + hz < 27; Neg[a] has the lanes whose offset along
@@ -97,6 +105,26 @@ template <> struct DiskAddr<false> {
     static constexpr uint32_t kUnit = 1;   // offsets in floats
     __device__ static __forceinline__ float ld(const float* b, uint32_t off) { return b[(uint64_t)off]; }
 };
+
+// Philox4x32-10 with the host-computed key schedule (bit-identical to pmc_philox4x32_10: round
+// r uses key (k0 + r*W0, k1 + r*W1)); fully unrolled, the keys are SGPR operands.
+__device__ __forceinline__ pmc_u32x4 philox_sched(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                                  const DevGeom& g) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)PMC_PHILOX_M0 * (uint64_t)c0;
+        const uint64_t p1 = (uint64_t)PMC_PHILOX_M1 * (uint64_t)c2;
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ g.rk0[r];
+        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ g.rk1[r];
+        c1 = (uint32_t)p1;
+        c3 = (uint32_t)p0;
+        c0 = n0;
+        c2 = n2;
+    }
+    pmc_u32x4 out;
+    out.v[0] = c0; out.v[1] = c1; out.v[2] = c2; out.v[3] = c3;
+    return out;
+}
 
 // exact n / d for 32-bit n (Granlund-Montgomery round-up method; magic from make_udiv_magic)
 __device__ __forceinline__ uint32_t udiv_magic(uint32_t n, UDivMagic m) {
@@ -162,7 +190,6 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     const int plane = g.cps_x * g.cps_y;
     const uint32_t c = (uint32_t)(x + g.cps_x * y + plane * (zl + g.halo));
     const uint32_t id = (uint32_t)x + (uint32_t)g.cps_x * ((uint32_t)y + (uint32_t)g.cps_y * (uint32_t)zg0);
-    const uint32_t k0 = g.k0, k1 = g.k1;
     const uint32_t row = (uint32_t)(3 * nm);                 // floats per cell
 
     // ---- 1. stencil table (lane k < 27; lanes >= 27 compute some in-range cell, unused) -------
@@ -170,14 +197,15 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     const int dx = (int)bit_of(kStencilPos[0], lane) - (int)bit_of(kStencilNeg[0], lane);
     const int dy = (int)bit_of(kStencilPos[1], lane) - (int)bit_of(kStencilNeg[1], lane);
     const int dz = (int)bit_of(kStencilPos[2], lane) - (int)bit_of(kStencilNeg[2], lane);
-    float k_sx = 0.0f, k_sy = 0.0f, k_sz = 0.0f;
-    int nx = x + dx, ny = y + dy;
-    if (nx < 0) { nx += g.cps_x; k_sx = -g.Lx; } else if (nx >= g.cps_x) { nx -= g.cps_x; k_sx = g.Lx; }
-    if (ny < 0) { ny += g.cps_y; k_sy = -g.Ly; } else if (ny >= g.cps_y) { ny -= g.cps_y; k_sy = g.Ly; }
-    const int zgn = zg0 + dz;
-    if (zgn < 0) k_sz = -g.Lz; else if (zgn >= g.cps_z) k_sz = g.Lz;
-    int nzl = zl + dz;
-    if (!g.halo) nzl = nzl < 0 ? nzl + g.cps_z : (nzl >= g.cps_z ? nzl - g.cps_z : nzl);
+    // periodic wrap as selects (no exec-mask branches)
+    const int nx0 = x + dx, ny0 = y + dy, zgn = zg0 + dz;
+    const int nx = nx0 + (nx0 < 0 ? g.cps_x : 0) - (nx0 >= g.cps_x ? g.cps_x : 0);
+    const int ny = ny0 + (ny0 < 0 ? g.cps_y : 0) - (ny0 >= g.cps_y ? g.cps_y : 0);
+    const float k_sx = nx0 < 0 ? -g.Lx : (nx0 >= g.cps_x ? g.Lx : 0.0f);
+    const float k_sy = ny0 < 0 ? -g.Ly : (ny0 >= g.cps_y ? g.Ly : 0.0f);
+    const float k_sz = zgn < 0 ? -g.Lz : (zgn >= g.cps_z ? g.Lz : 0.0f);
+    const int nz0 = zl + dz;
+    const int nzl = g.halo ? nz0 : nz0 + (nz0 < 0 ? g.cps_z : 0) - (nz0 >= g.cps_z ? g.cps_z : 0);
     const uint32_t kc = (uint32_t)(nx + g.cps_x * ny + plane * (nzl + g.halo));
     const int k_cnt = ncnt[kc];
     const uint32_t k_off = kc * row * DiskAddr<OFF32>::kUnit;   // bytes (OFF32) or floats
@@ -212,7 +240,7 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
         if (lane < 16) { idx = (uint32_t)(m0 + lane); tag = PMC_TAG_MOVE; }
         else if (lane < 32) { idx = (uint32_t)(m0 + lane - 16); tag = PMC_TAG_ACCEPT; }
         else { idx = (uint32_t)(lane - 32); tag = PMC_TAG_SHUFFLE; }
-        const pmc_u32x4 w = pmc_philox4x32_10(idx, id, sweep, tag, k0, k1);
+        const pmc_u32x4 w = philox_sched(idx, id, sweep, tag, g);
         if (first) {
             const int jraw = (int)pmc_bounded(w.v[0], (uint32_t)(lane - 32 + 1));
             jv = __shfl(jraw, (lane + 32) & 63);                  // slot i's FY index in lane i
@@ -235,7 +263,7 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     if (n_own == 0) return true;                                // subsweep.h:252-253
     const int cap_nb = cap - n_own;
     if (n_own > 32) {     // nmax > 32: Fisher-Yates words of slots 32..63
-        const pmc_u32x4 w = pmc_philox4x32_10((uint32_t)lane, id, sweep, PMC_TAG_SHUFFLE, k0, k1);
+        const pmc_u32x4 w = philox_sched((uint32_t)lane, id, sweep, PMC_TAG_SHUFFLE, g);
         if (lane >= 32) jv = (int)pmc_bounded(w.v[0], (uint32_t)(lane + 1));
     }
 
@@ -276,8 +304,7 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
             const int nk = wave_uniform(__popcll(mk));
             if (S_nb + nk <= cap_nb) {            // otherwise the cell goes to the fallback
                 // unconditional stores, discarded lanes into the row tails (>= 32 slots)
-                const int slot = __builtin_amdgcn_inverse_ballot_w64(mk) ? S_nb + mbcnt64(mk)
-                                                                        : stride - 32 + (lane & 31);
+                const int slot = select_by_mask(mk, S_nb + mbcnt64(mk), stride - 32 + (lane & 31));
                 float* dst = px_ + slot;
                 dst[0] = ux;
                 dst[stride] = uy;
@@ -360,10 +387,8 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
                     const unsigned long long mn = __builtin_amdgcn_ballot_w64(r2n <= rc2);
                     const unsigned long long mo = __builtin_amdgcn_ballot_w64(r2o <= rc2);
                     const int cn = C + __popcll(mn);
-                    const int dn = __builtin_amdgcn_inverse_ballot_w64(mn) ? C + mbcnt64(mn) : 2 * lcap + lane;
-                    buf[dn] = r2n;
-                    const int dO = __builtin_amdgcn_inverse_ballot_w64(mo) ? cn + mbcnt64(mo) : 2 * lcap + lane;
-                    buf[dO] = -r2o;
+                    buf[select_by_mask(mn, C + mbcnt64(mn), 2 * lcap + lane)] = r2n;
+                    buf[select_by_mask(mo, cn + mbcnt64(mo), 2 * lcap + lane)] = -r2o;
                     C = cn + __popcll(mo);
                 };
                 block(0);
