@@ -156,9 +156,15 @@ PMC_HD float pmc_accept_threshold(pmc_u32x4 w) { return -pmc_logf(pmc_u01(w.v[0]
 /* ------------------------------------------------------------------------------------- */
 #define PMC_R2_MIN 1.0e-4f
 
+/* r2 = fma(dz, dz, fma(dy, dy, dx*dx)): one multiply and two fused multiply-adds (v_mul +
+ * 2 v_fma on gfx950, vmulss + 2 vfmadd on x86-64-v3), each a single IEEE rounding, so host and
+ * device agree bit for bit.  Round-to-nearest is symmetric under negation, so
+ * pmc_r2_neg = -pmc_r2 exactly (the kernels list old-position terms negated at no cost). */
 PMC_HD float pmc_r2(float dx, float dy, float dz) {
-    float r2 = dx * dx + dy * dy;
-    return r2 + dz * dz;
+    return __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx));
+}
+PMC_HD float pmc_r2_neg(float dx, float dy, float dz) {
+    return __builtin_fmaf(-dz, dz, __builtin_fmaf(-dy, dy, (-dx) * dx));
 }
 
 /* Reciprocal by three Newton-Raphson steps from a bit-trick seed (max seed error 5.1%,
@@ -216,8 +222,7 @@ PMC_HD float pmc_box_d2(float x, float y, float z, const float lo[3], const floa
     float tx = __builtin_fmaxf(__builtin_fmaxf(lo[0] - x, x - hi[0]), 0.0f);
     float ty = __builtin_fmaxf(__builtin_fmaxf(lo[1] - y, y - hi[1]), 0.0f);
     float tz = __builtin_fmaxf(__builtin_fmaxf(lo[2] - z, z - hi[2]), 0.0f);
-    float d2 = tx * tx + ty * ty;
-    return d2 + tz * tz;
+    return pmc_r2(tx, ty, tz);
 }
 
 /* own-cell closed box padded by PMC_BOX_PAD: lb = c*w - L/2.0f (start.cu:129), ub = lb + w */

@@ -341,6 +341,7 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     const float czf = (float)zg0 * g.w - g.Lz / 2.0f + hw;
     const double beta_d = (double)g.beta;
     const float rc2 = g.rc2;
+    const float nrc2 = -g.rc2;
     // PMC_R2_MIN through an SGPR: v_max_f32 |r2s|, s takes it with the free |.| modifier (a
     // literal operand would force a second max)
     const float r2min = as_f(wave_uniform(as_i(g.r2min)));
@@ -382,13 +383,15 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
                     // slots >= K and the moving slot hold +inf in x: their r2 is inf, never listed
                     const int k = base + lane;
                     const float xj = px_[k], yj = py_[k], zj = pz_[k];
+                    // old-position term computed negated (= -r2o bit for bit, pmc_r2_neg):
+                    // listed with its sign bit set at no extra instruction
                     const float r2n = pmc_r2(qx - xj, qy - yj, qz - zj);
-                    const float r2o = pmc_r2(xi - xj, yi - yj, zi - zj);
+                    const float r2on = pmc_r2_neg(xi - xj, yi - yj, zi - zj);
                     const unsigned long long mn = __builtin_amdgcn_ballot_w64(r2n <= rc2);
-                    const unsigned long long mo = __builtin_amdgcn_ballot_w64(r2o <= rc2);
+                    const unsigned long long mo = __builtin_amdgcn_ballot_w64(r2on >= nrc2);
                     const int cn = C + __popcll(mn);
-                    buf[select_by_mask(mn, C + mbcnt64(mn), 2 * lcap + lane)] = r2n;
-                    buf[select_by_mask(mo, cn + mbcnt64(mo), 2 * lcap + lane)] = -r2o;
+                    buf[select_by_mask(mn, mbcnt64_add(mn, C), 2 * lcap + lane)] = r2n;
+                    buf[select_by_mask(mo, mbcnt64_add(mo, cn), 2 * lcap + lane)] = r2on;
                     C = cn + __popcll(mo);
                 };
                 block(0);
