@@ -189,8 +189,10 @@ int pmc_create(const pmc_params* params, pmc_ctx** out) {
     if ((e = hipMalloc(&c->flags, 16)) != hipSuccess) return cleanup(hip_fail(e, "hipMalloc flags"));
     {
         const size_t per_colour = (size_t)(p.cps_x / 2) * (p.cps_y / 2) * (p.nz_local / 2);
-        if ((e = hipMalloc(&c->ovf, sizeof(int) * (1 + per_colour))) != hipSuccess)
-            return cleanup(hip_fail(e, "hipMalloc ovf"));
+        // header (queue length, done counter: zero between launches) + one entry per cell
+        const size_t ob = sizeof(int) * (kOvfHead + per_colour);
+        if ((e = hipMalloc(&c->ovf, ob)) != hipSuccess) return cleanup(hip_fail(e, "hipMalloc ovf"));
+        if ((e = hipMemset(c->ovf, 0, ob)) != hipSuccess) return cleanup(hip_fail(e, "hipMemset"));
     }
     if ((e = hipMemset(c->flags, 0, 16)) != hipSuccess) return cleanup(hip_fail(e, "hipMemset"));
     if ((e = hipEventCreate(&c->ev0)) != hipSuccess) return cleanup(hip_fail(e, "hipEventCreate"));

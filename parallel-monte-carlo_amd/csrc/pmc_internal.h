@@ -22,7 +22,8 @@ __host__ __device__ constexpr int subsweep_stride(int lcap) { return (lcap + 32 
 __host__ __device__ constexpr int lds_floats_per_wave(int lcap) { return 3 * subsweep_stride(lcap) + 2 * lcap + 64; }
 constexpr int kMainCap = 224;       // main launch: lds_floats_per_wave(224) * 4 B = 5120 B (32 waves/CU)
 static_assert(lds_floats_per_wave(kMainCap) * 4 <= 5120, "main-launch LDS per wave");
-constexpr int kStatCounters = 4;   // de_fixed, accepted, trials, evaluated
+constexpr int kStatCounters = 4;
+constexpr int kOvfHead = 2;       // ints of the subsweep overflow-queue header (pmc_kernels.hip)   // de_fixed, accepted, trials, evaluated
 
 // Unsigned division by an invariant d: n / d = (hi + ((n - hi) >> sh1)) >> sh2, hi = umulhi(n, mul)
 // (Granlund & Montgomery 1994, round-up variant; exact for every 32-bit n).

@@ -23,6 +23,21 @@
 
 namespace pmc {
 
+#ifdef PMC_STAMPS
+// Analysis build only (-DPMC_STAMPS, tools/stamps.py): per-wave s_memtime stamps at the section
+// boundaries of a main-launch cell visit, written by lane 0 with vector stores.
+__device__ unsigned long long* g_stamps = nullptr;
+#define PMC_STAMP(k)                                                                              \
+    do {                                                                                          \
+        if (LCAP == kMainCap && g_stamps && lane == 0)                                            \
+            g_stamps[(size_t)t * 8 + (k)] = __builtin_amdgcn_s_memtime();                        \
+    } while (0)
+#else
+#define PMC_STAMP(k) \
+    do {             \
+    } while (0)
+#endif
+
 namespace {
 
 __device__ __forceinline__ float as_f(int v) { return __builtin_bit_cast(float, v); }
@@ -192,6 +207,7 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     const uint32_t id = (uint32_t)x + (uint32_t)g.cps_x * ((uint32_t)y + (uint32_t)g.cps_y * (uint32_t)zg0);
     const uint32_t row = (uint32_t)(3 * nm);                 // floats per cell
 
+    PMC_STAMP(0);
     // ---- 1. stencil table (lane k < 27; lanes >= 27 compute some in-range cell, unused) -------
     // lane k = 9*hx + 3*hy + hz, h = 0, 1, 2 -> offset 0, -1, +1 (get_neighbors order)
     const int dx = (int)bit_of(kStencilPos[0], lane) - (int)bit_of(kStencilNeg[0], lane);
@@ -232,6 +248,7 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
         ownz = own[2 * nm + l];
     }
 
+    PMC_STAMP(1);
     // ---- 2. random numbers for the first 16 moves + the shuffle (overlaps the loads) ------------
     float G0 = 0.0f, G1 = 0.0f, TT = 0.0f;
     int jv = 0;
@@ -258,9 +275,11 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
         TT = -lg;         // lanes 16-31: acceptance threshold of move m0+lane-16
     };
     rng_chunk(0, true);
+    PMC_STAMP(2);
 
     const int n_own = __builtin_amdgcn_readfirstlane(k_cnt);   // lane 0 = own cell
     if (n_own == 0) return true;                                // subsweep.h:252-253
+    PMC_STAMP(3);
     const int cap_nb = cap - n_own;
     if (n_own > 32) {     // nmax > 32: Fisher-Yates words of slots 32..63
         const pmc_u32x4 w = philox_sched((uint32_t)lane, id, sweep, PMC_TAG_SHUFFLE, g);
@@ -268,14 +287,29 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     }
 
     // ---- Fisher-Yates shuffle of the own cell (random_shuffle, subsweep.h:50-58; fixes R1) ---
-    int perm = lane;
-    for (int i = n_own - 1; i > 0; --i) {
-        const int j = __builtin_amdgcn_readlane(jv, i);
-        const int vi = __builtin_amdgcn_readlane(perm, i);
-        const int vj = __builtin_amdgcn_readlane(perm, j);
-        perm = lane == i ? vj : (lane == j ? vi : perm);
+    int perm;
+    if (n_own <= 16) {
+        // the permutation as 16 nibbles of one 64-bit scalar: each swap is a few SALU ops on
+        // SGPRs (no VGPR read-modify-write chain through v_readlane), one VALU unpack at the end
+        uint64_t P = 0xFEDCBA9876543210ull;
+        for (int i = n_own - 1; i > 0; --i) {
+            const uint32_t j = (uint32_t)__builtin_amdgcn_readlane(jv, i);
+            const uint32_t si = 4u * (uint32_t)i, sj = 4u * j;
+            const uint64_t d = ((P >> si) ^ (P >> sj)) & 15u;   // a[i] ^ a[j]
+            P ^= (d << si) | (d << sj);                        // swap (d == 0 when i == j)
+        }
+        perm = (int)((P >> (4u * (uint32_t)(lane & 15))) & 15u);
+    } else {
+        perm = lane;
+        for (int i = n_own - 1; i > 0; --i) {
+            const int j = __builtin_amdgcn_readlane(jv, i);
+            const int vi = __builtin_amdgcn_readlane(perm, i);
+            const int vj = __builtin_amdgcn_readlane(perm, j);
+            perm = lane == i ? vj : (lane == j ? vi : perm);
+        }
     }
 
+    PMC_STAMP(4);
     // ---- 3. stage neighbours (filtered, compacted) then the own cell -------------------------
     float blo[3], bhi[3];
     pmc_cell_box(x, y, zg0, g.w, g.Lx, g.Ly, g.Lz, blo, bhi);
@@ -334,6 +368,7 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     const float kFar = __builtin_inff();
     px_[(K + lane) < stride ? K + lane : stride - 1] = kFar;
 
+    PMC_STAMP(5);
     // cell centre for out_of_bound (subsweep.h:73-88): c*w - L/2 + w/2 in float
     const float hw = g.w / 2.0f;
     const float cxf = (float)x * g.w - g.Lx / 2.0f + hw;
@@ -425,6 +460,7 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
         }
     }
 
+    PMC_STAMP(6);
     // ---- 5. write back the own cell in shuffled order (cpy_D_sh_to_Disk, subsweep.h:29-36) ----
     if (lane < n_own) {
         const uint32_t off = c * (uint32_t)(3 * nm) + (uint32_t)lane;
@@ -439,8 +475,13 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
         atomicAdd(&stats[2 * kStatSlots + slot], (unsigned long long)g.n_moves);
         atomicAdd(&stats[3 * kStatSlots + slot], (unsigned long long)n_ev);
     }
+    PMC_STAMP(7);
     return true;
 }
+
+// Overflow queue header (ints): [kOvfCount] queued cells, [kOvfDone] fallback workgroups done;
+// entries from kOvfHead.  Zero between launches (the fallback's last workgroup resets it).
+constexpr int kOvfCount = 0, kOvfDone = 1;
 
 // Main launch: one wave per cell of the colour; LDS layout for kMainCap partners, capacity `cap`
 // (<= kMainCap) partners per wave (sized for the occupancy; a cell whose filtered stencil
@@ -463,7 +504,7 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep(DevGeom g, float
     if (t >= total) return;
     if (!subsweep_wave<NSLOT, NMC, kMainCap, OFF32>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, kMainCap, cap,
                                                 t, cz0)) {
-        if ((threadIdx.x & (kWave - 1)) == 0) ovf[1 + atomicAdd(&ovf[0], 1)] = t;
+        if ((threadIdx.x & (kWave - 1)) == 0) ovf[kOvfHead + atomicAdd(&ovf[kOvfCount], 1)] = t;
     }
 }
 
@@ -479,11 +520,21 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_fallback(DevGeom
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int full = 27 * (NMC > 0 ? NMC : g.nmax);
     float* px_ = smem + wv * lds_floats_per_wave(full);
-    const int count = __builtin_amdgcn_readfirstlane(ovf[0]);
+    const int count = __builtin_amdgcn_readfirstlane(ovf[kOvfCount]);
     for (int e = (int)blockIdx.x * kSubWaves + wv; e < count; e += (int)gridDim.x * kSubWaves) {
-        const int t = __builtin_amdgcn_readfirstlane(ovf[1 + e]);
+        const int t = __builtin_amdgcn_readfirstlane(ovf[kOvfHead + e]);
         (void)subsweep_wave<NSLOT, NMC, 27 * NMC, OFF32>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, full, full, t,
                                                   cz0);
+    }
+    // the last workgroup to finish (every workgroup has read the count by then) clears the queue
+    // for the next launch: no memset between launches, and graph replays start from a clean queue
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(&ovf[kOvfDone], 1) == (int)gridDim.x - 1) {
+            ovf[kOvfCount] = 0;
+            ovf[kOvfDone] = 0;
+        }
     }
 }
 
@@ -791,8 +842,6 @@ hipError_t launch_subsweep(const DevGeom& g, float* disk, const int16_t* n, int 
     if (cz1 > nczc) cz1 = nczc;
     if (cz1 <= cz0) return hipSuccess;
     const int ncz = cz1 - cz0;
-    hipError_t e = hipMemsetAsync(ovf, 0, sizeof(int), st);
-    if (e != hipSuccess) return e;
     // 32-bit byte offsets when the disk buffer is below 4 GiB (every single-GPU 256^3 config)
     // (test hook: PMC_FORCE_ADDR64 takes the 64-bit path for any size)
     static const bool force64 = std::getenv("PMC_FORCE_ADDR64") != nullptr;
@@ -862,3 +911,23 @@ hipError_t launch_selftest(const uint32_t* words, int count, float* out_f, doubl
 }
 
 }  // namespace pmc
+
+#ifdef PMC_STAMPS
+extern "C" int pmc_debug_stamps(size_t n_cells, unsigned long long* host_out) {
+    static unsigned long long* buf = nullptr;
+    static size_t cap = 0;
+    if (host_out == nullptr) {   // enable (allocate + zero) for n_cells colour cells
+        if (n_cells > cap) {
+            if (buf) (void)hipFree(buf);
+            if (hipMalloc(&buf, n_cells * 8 * sizeof(unsigned long long)) != hipSuccess) return -2;
+            cap = n_cells;
+        }
+        if (hipMemset(buf, 0, n_cells * 8 * sizeof(unsigned long long)) != hipSuccess) return -2;
+        return hipMemcpyToSymbol(HIP_SYMBOL(pmc::g_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : -2;
+    }
+    if (hipDeviceSynchronize() != hipSuccess) return -2;
+    if (hipMemcpy(host_out, buf, n_cells * 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) return -2;
+    unsigned long long* null = nullptr;   // disable
+    return hipMemcpyToSymbol(HIP_SYMBOL(pmc::g_stamps), &null, sizeof(null)) == hipSuccess ? 0 : -2;
+}
+#endif

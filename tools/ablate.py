@@ -18,13 +18,16 @@ for nm in [int(v) for v in os.environ.get("MOVES", "0,1,5,10,20").split(",")]:
     for s in range(2):
         ctx.sweep(s)
     ctx.synchronize()
-    t0 = time.perf_counter()
-    reps = 5
+    reps = int(os.environ.get("REPS", "5"))
+    times = []
     for s in range(reps):
+        t0 = time.perf_counter()
         for c in range(8):
             ctx.phase(c, 100 + s)
-    ctx.synchronize()
-    dt = (time.perf_counter() - t0) / (reps * 8)
+        ctx.synchronize()
+        times.append((time.perf_counter() - t0) / 8)
+    times.sort()
+    dt = times[len(times) // 2]
     st = ctx.stats()
     print(f"n_moves={nm:3d}  phase_ms={dt*1e3:.4f}  evaluated/trials={st['evaluated']/max(1,st['trials']):.3f}", flush=True)
     ctx.close()
