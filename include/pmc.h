@@ -168,6 +168,43 @@ int pmc_plane_span(const pmc_ctx* ctx, int z_local, size_t* disk_off, size_t* di
  * host == device bit equality of every transcendental the kernels use. */
 int pmc_selftest_detmath(const uint32_t* h_words, int count, float* h_out_f, double* h_out_d);
 
+/* ---- trajectory dump / restart ---------------------------------- */
+/* The reference's visualisation path is host code: disk_to_r + create_dump
+ * (CUDA-Parallel-MC/CUDA-Parallel-MC/kernel.cu:497-536), LAMMPS-style text for OVITO.  It has
+ * no reader and no checkpoint; the reader and the binary snapshot below are the restart path.
+ * The host-only functions need no GPU. */
+/* disk_to_r (kernel.cu:500-510): particles of `cells` cells in cell order, then slot order, into
+ * h_r[3*stride] (SoA: x at [0,stride), y at [stride,2*stride), z after).  h_r == NULL only counts.
+ * *count = particles found; PMC_ERR_ARG if they exceed stride or a count is outside [0, nmax]. */
+int pmc_disk_to_r(const float* h_disk, const int16_t* h_n, int64_t cells, int32_t nmax, float* h_r,
+                  int64_t stride, int64_t* count);
+/* One frame in create_dump's format (kernel.cu:521-535): "ITEM: TIMESTEP \n<t>\n ITEM: NUMBER OF
+ * ATOMS ... ITEM: BOX BOUNDS ... ITEM: ATOMS id type x y z ix iy iz", coordinates "%f", ids 1..n.
+ * append = 0 truncates the file. */
+int pmc_write_dump(const char* path, int append, int64_t timestep, const float* h_r, int64_t stride,
+                   int64_t n_atoms, const float box_lo[3], const float box_hi[3]);
+/* Read frame `frame` (0-based) of such a file into h_r[3*stride] by atom id; h_r == NULL reads the
+ * header only (timestep, n_atoms, box).  PMC_ERR_RANGE if the file has fewer frames. */
+int pmc_read_dump(const char* path, int64_t frame, int64_t* timestep, float* h_r, int64_t stride,
+                  int64_t* n_atoms, float box_lo[3], float box_hi[3]);
+/* Binary snapshot "PMCSNAP1": parameters, the next sweep index (the whole RNG state: Philox
+ * counters are (sweep, cell, move)), the accumulated statistics, and every occupied slot's
+ * exact float bits; FNV-1a checksum; written to path.tmp then renamed.  h_disk/h_n hold `cells`
+ * cells in the reference layout (pmc_snapshot_read zero-fills unused slots; h_disk == h_n == NULL
+ * reads the header only). */
+int pmc_snapshot_write(const char* path, const pmc_params* params, uint32_t next_sweep,
+                       const pmc_stats* stats, const float* h_disk, const int16_t* h_n, int64_t cells);
+int pmc_snapshot_read(const char* path, pmc_params* params, uint32_t* next_sweep, pmc_stats* stats,
+                      float* h_disk, int16_t* h_n, int64_t cells);
+/* Context wrappers (owned cells; slab mode: this rank's planes, halos must be exchanged after a
+ * load).  pmc_dump_frame writes the current state as one frame with box -L/2..L/2 per axis. */
+int pmc_get_params(const pmc_ctx* ctx, pmc_params* out);
+int pmc_stats_write(pmc_ctx* ctx, const pmc_stats* in);
+int pmc_dump_frame(pmc_ctx* ctx, const char* path, int append, int64_t timestep);
+int pmc_save_snapshot(pmc_ctx* ctx, const char* path, uint32_t next_sweep);
+/* Restores state + statistics; PMC_ERR_ARG if the snapshot's parameters differ from the ctx's. */
+int pmc_load_snapshot(pmc_ctx* ctx, const char* path, uint32_t* next_sweep);
+
 #ifdef __cplusplus
 }
 #endif

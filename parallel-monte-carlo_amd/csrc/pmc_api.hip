@@ -157,6 +157,9 @@ extern "C" {
 
 const char* pmc_last_error(void) { return g_err.c_str(); }
 
+// error reporting for the host-only I/O functions (pmc_io.cpp); internal, not in pmc.h
+int pmc_io_fail(int code, const char* msg) { return fail(code, msg); }
+
 int pmc_create(const pmc_params* params, pmc_ctx** out) {
     if (!params || !out) return fail(PMC_ERR_ARG, "null argument");
     *out = nullptr;
@@ -524,3 +527,90 @@ int pmc_selftest_detmath(const uint32_t* h_words, int count, float* h_out_f, dou
 }
 
 }  // extern "C"
+
+// ---- trajectory dump / restart (kernel.cu:497-536; pmc_io.cpp holds the host formats) ----------
+namespace {
+
+// owned cells of the storage (slab mode skips the halo planes)
+void owned_range(const pmc_ctx* c, int64_t* first, int64_t* count) {
+    const int64_t plane = (int64_t)c->P.cps_x * c->P.cps_y;
+    *first = c->P.halo ? plane : 0;
+    *count = plane * c->P.nz_local;
+}
+
+}  // namespace
+
+int pmc_get_params(const pmc_ctx* c, pmc_params* out) {
+    if (!c || !out) return fail(PMC_ERR_ARG, "bad argument");
+    *out = c->P;
+    return PMC_OK;
+}
+
+int pmc_stats_write(pmc_ctx* c, const pmc_stats* in) {
+    if (!c || !in) return fail(PMC_ERR_ARG, "bad argument");
+    std::vector<unsigned long long> h((size_t)kStatCounters * kStatSlots, 0ull);
+    h[0 * kStatSlots] = (unsigned long long)in->de_fixed;
+    h[1 * kStatSlots] = (unsigned long long)in->accepted;
+    h[2 * kStatSlots] = (unsigned long long)in->trials;
+    h[3 * kStatSlots] = (unsigned long long)in->evaluated;
+    PMC_HIP(hipMemcpyAsync(c->stats, h.data(), sizeof(unsigned long long) * h.size(), hipMemcpyHostToDevice, c->stream));
+    PMC_HIP(hipStreamSynchronize(c->stream));
+    return PMC_OK;
+}
+
+int pmc_dump_frame(pmc_ctx* c, const char* path, int append, int64_t timestep) {
+    if (!c || !path) return fail(PMC_ERR_ARG, "bad argument");
+    std::vector<float> disk((size_t)c->cells * 3 * (size_t)c->P.nmax);
+    std::vector<int16_t> n((size_t)c->cells);
+    int rc = pmc_copy_out(c, disk.data(), n.data());
+    if (rc) return rc;
+    int64_t first, count, atoms = 0;
+    owned_range(c, &first, &count);
+    const float* d0 = disk.data() + (size_t)first * 3 * (size_t)c->P.nmax;
+    if ((rc = pmc_disk_to_r(d0, n.data() + first, count, c->P.nmax, nullptr, 0, &atoms))) return rc;
+    std::vector<float> r((size_t)atoms * 3);
+    if ((rc = pmc_disk_to_r(d0, n.data() + first, count, c->P.nmax, r.data(), atoms, &atoms))) return rc;
+    // the reference writes -L/2 .. L/2 on every axis (kernel.cu:523-524); global box in slab mode
+    const float lo[3] = {-c->G.Lx / 2.0f, -c->G.Ly / 2.0f, -c->G.Lz / 2.0f};
+    const float hi[3] = {c->G.Lx / 2.0f, c->G.Ly / 2.0f, c->G.Lz / 2.0f};
+    return pmc_write_dump(path, append, timestep, r.data(), atoms, atoms, lo, hi);
+}
+
+int pmc_save_snapshot(pmc_ctx* c, const char* path, uint32_t next_sweep) {
+    if (!c || !path) return fail(PMC_ERR_ARG, "bad argument");
+    std::vector<float> disk((size_t)c->cells * 3 * (size_t)c->P.nmax);
+    std::vector<int16_t> n((size_t)c->cells);
+    int rc = pmc_copy_out(c, disk.data(), n.data());
+    if (rc) return rc;
+    pmc_stats st;
+    if ((rc = pmc_stats_read(c, &st, 0))) return rc;
+    int64_t first, count;
+    owned_range(c, &first, &count);
+    return pmc_snapshot_write(path, &c->P, next_sweep, &st, disk.data() + (size_t)first * 3 * (size_t)c->P.nmax,
+                              n.data() + first, count);
+}
+
+int pmc_load_snapshot(pmc_ctx* c, const char* path, uint32_t* next_sweep) {
+    if (!c || !path) return fail(PMC_ERR_ARG, "bad argument");
+    pmc_params q;
+    uint32_t sw = 0;
+    pmc_stats st;
+    int rc = pmc_snapshot_read(path, &q, &sw, &st, nullptr, nullptr, 0);
+    if (rc) return rc;
+    const pmc_params& p = c->P;
+    if (q.cps_x != p.cps_x || q.cps_y != p.cps_y || q.cps_z != p.cps_z || q.nz_local != p.nz_local || q.z0 != p.z0 ||
+        q.halo != p.halo || q.nmax != p.nmax || q.n_moves != p.n_moves || q.w != p.w || q.beta != p.beta ||
+        q.sigma != p.sigma || q.seed != p.seed)
+        return fail(PMC_ERR_ARG, "pmc_load_snapshot: snapshot parameters differ from the context's");
+    int64_t first, count;
+    owned_range(c, &first, &count);
+    std::vector<float> disk((size_t)c->cells * 3 * (size_t)p.nmax, 0.0f);
+    std::vector<int16_t> n((size_t)c->cells, 0);
+    if ((rc = pmc_snapshot_read(path, nullptr, nullptr, nullptr, disk.data() + (size_t)first * 3 * (size_t)p.nmax,
+                                n.data() + first, count)))
+        return rc;
+    if ((rc = pmc_copy_in(c, disk.data(), n.data()))) return rc;   // halo planes: zero until exchanged
+    if ((rc = pmc_stats_write(c, &st))) return rc;
+    if (next_sweep) *next_sweep = sw;
+    return PMC_OK;
+}

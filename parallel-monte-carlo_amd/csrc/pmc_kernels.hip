@@ -30,7 +30,7 @@ __device__ unsigned long long* g_stamps = nullptr;
 #define PMC_STAMP(k)                                                                              \
     do {                                                                                          \
         if (LCAP == kMainCap && g_stamps && lane == 0)                                            \
-            g_stamps[(size_t)t * 8 + (k)] = __builtin_amdgcn_s_memtime();                        \
+            g_stamps[(size_t)t * 16 + (k)] = __builtin_amdgcn_s_memtime();                        \
     } while (0)
 #else
 #define PMC_STAMP(k) \
@@ -230,6 +230,7 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     const int pp = p < nm ? p : 0;
     const uint32_t pp_off = (uint32_t)pp * DiskAddr<OFF32>::kUnit;
     const uint32_t nm_off = (uint32_t)nm * DiskAddr<OFF32>::kUnit;
+    PMC_STAMP(1);
     float vx[NP], vy[NP], vz[NP];
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
@@ -248,7 +249,7 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
         ownz = own[2 * nm + l];
     }
 
-    PMC_STAMP(1);
+    PMC_STAMP(2);
     // ---- 2. random numbers for the first 16 moves + the shuffle (overlaps the loads) ------------
     float G0 = 0.0f, G1 = 0.0f, TT = 0.0f;
     int jv = 0;
@@ -275,11 +276,11 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
         TT = -lg;         // lanes 16-31: acceptance threshold of move m0+lane-16
     };
     rng_chunk(0, true);
-    PMC_STAMP(2);
+    PMC_STAMP(3);
 
     const int n_own = __builtin_amdgcn_readfirstlane(k_cnt);   // lane 0 = own cell
     if (n_own == 0) return true;                                // subsweep.h:252-253
-    PMC_STAMP(3);
+    PMC_STAMP(4);
     const int cap_nb = cap - n_own;
     if (n_own > 32) {     // nmax > 32: Fisher-Yates words of slots 32..63
         const pmc_u32x4 w = philox_sched((uint32_t)lane, id, sweep, PMC_TAG_SHUFFLE, g);
@@ -309,7 +310,7 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
         }
     }
 
-    PMC_STAMP(4);
+    PMC_STAMP(5);
     // ---- 3. stage neighbours (filtered, compacted) then the own cell -------------------------
     float blo[3], bhi[3];
     pmc_cell_box(x, y, zg0, g.w, g.Lx, g.Ly, g.Lz, blo, bhi);
@@ -349,6 +350,7 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     };
     if (edge) stage(std::true_type{});
     else stage(std::false_type{});
+    PMC_STAMP(6);
     S_nb = wave_uniform(S_nb);   // keep it scalar past the divergent stores (structurizer joins)
     if (S_nb > cap_nb) return false;                            // -> full-capacity fallback
     {
@@ -368,7 +370,7 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     const float kFar = __builtin_inff();
     px_[(K + lane) < stride ? K + lane : stride - 1] = kFar;
 
-    PMC_STAMP(5);
+    PMC_STAMP(7);
     // cell centre for out_of_bound (subsweep.h:73-88): c*w - L/2 + w/2 in float
     const float hw = g.w / 2.0f;
     const float cxf = (float)x * g.w - g.Lx / 2.0f + hw;
@@ -460,7 +462,7 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
         }
     }
 
-    PMC_STAMP(6);
+    PMC_STAMP(8);
     // ---- 5. write back the own cell in shuffled order (cpy_D_sh_to_Disk, subsweep.h:29-36) ----
     if (lane < n_own) {
         const uint32_t off = c * (uint32_t)(3 * nm) + (uint32_t)lane;
@@ -475,7 +477,7 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
         atomicAdd(&stats[2 * kStatSlots + slot], (unsigned long long)g.n_moves);
         atomicAdd(&stats[3 * kStatSlots + slot], (unsigned long long)n_ev);
     }
-    PMC_STAMP(7);
+    PMC_STAMP(9);
     return true;
 }
 
@@ -919,14 +921,14 @@ extern "C" int pmc_debug_stamps(size_t n_cells, unsigned long long* host_out) {
     if (host_out == nullptr) {   // enable (allocate + zero) for n_cells colour cells
         if (n_cells > cap) {
             if (buf) (void)hipFree(buf);
-            if (hipMalloc(&buf, n_cells * 8 * sizeof(unsigned long long)) != hipSuccess) return -2;
+            if (hipMalloc(&buf, n_cells * 16 * sizeof(unsigned long long)) != hipSuccess) return -2;
             cap = n_cells;
         }
-        if (hipMemset(buf, 0, n_cells * 8 * sizeof(unsigned long long)) != hipSuccess) return -2;
+        if (hipMemset(buf, 0, n_cells * 16 * sizeof(unsigned long long)) != hipSuccess) return -2;
         return hipMemcpyToSymbol(HIP_SYMBOL(pmc::g_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : -2;
     }
     if (hipDeviceSynchronize() != hipSuccess) return -2;
-    if (hipMemcpy(host_out, buf, n_cells * 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) return -2;
+    if (hipMemcpy(host_out, buf, n_cells * 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) return -2;
     unsigned long long* null = nullptr;   // disable
     return hipMemcpyToSymbol(HIP_SYMBOL(pmc::g_stamps), &null, sizeof(null)) == hipSuccess ? 0 : -2;
 }

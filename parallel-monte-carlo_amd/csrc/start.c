@@ -4,6 +4,12 @@
  *
  *   start [--cps 4] [--atoms 64] [--passes 1000] [--nmax 16] [--moves 10] [--beta 0.3]
  *         [--sigma 0.5] [--w 2.5] [--seed 1234] [--every 1] [--graph]
+ *         [--dump FILE] [--save FILE] [--restart FILE]
+ *
+ * --dump writes create_dump frames (kernel.cu:510-536; the reference's VISUALISATION path) of the
+ * initial state and after every --every sweeps; --save writes a PMCSNAP1 snapshot at the end;
+ * --restart continues from a snapshot (its sweep index, state and statistics) instead of the
+ * lattice, for --passes further sweeps.
  *
  * Prints "step: energy" lines like kernel.cu:643,695 (energy from the cell-list sum every
  * --every sweeps) and a final summary with acceptance ratio and trial-moves/s.  Compile-time
@@ -27,6 +33,7 @@ int main(int argc, char** argv) {
     p.w = 2.5f; p.beta = 0.3f; p.sigma = 0.5f; p.seed = 1234;
     long long atoms = 64;
     int passes = 1000, every = 1, graph = 0;
+    const char *dump = NULL, *save = NULL, *restart = NULL;
     for (int i = 1; i < argc; ++i) {
         const char* a = argv[i];
         const char* v = (i + 1 < argc) ? argv[i + 1] : "0";
@@ -41,6 +48,9 @@ int main(int argc, char** argv) {
         else if (!strcmp(a, "--seed")) { p.seed = strtoull(v, NULL, 10); ++i; }
         else if (!strcmp(a, "--every")) { every = atoi(v); ++i; }
         else if (!strcmp(a, "--graph")) { graph = 1; }
+        else if (!strcmp(a, "--dump")) { dump = v; ++i; }
+        else if (!strcmp(a, "--save")) { save = v; ++i; }
+        else if (!strcmp(a, "--restart")) { restart = v; ++i; }
         else { fprintf(stderr, "unknown flag %s\n", a); return 2; }
     }
     if (every < 1) every = 1;
@@ -48,8 +58,13 @@ int main(int argc, char** argv) {
     pmc_ctx* ctx = NULL;
     int rc = pmc_create(&p, &ctx);
     if (rc) die("pmc_create", rc);
-    rc = pmc_init_lattice(ctx, atoms);
-    if (rc) die("pmc_init_lattice", rc);
+    uint32_t first = 0;
+    if (restart) {
+        if ((rc = pmc_load_snapshot(ctx, restart, &first))) die("pmc_load_snapshot", rc);
+    } else if ((rc = pmc_init_lattice(ctx, atoms))) {
+        die("pmc_init_lattice", rc);
+    }
+    if (dump && (rc = pmc_dump_frame(ctx, dump, 0, (int64_t)first))) die("pmc_dump_frame", rc);
 
     double e = 0.0;
     rc = pmc_energy(ctx, &e);
@@ -58,8 +73,9 @@ int main(int argc, char** argv) {
     pmc_stats total;
     memset(&total, 0, sizeof(total));
     double seconds = 0.0;
-    for (int s = 0; s < passes; s += every) {
-        int k = (passes - s) < every ? (passes - s) : every;
+    for (int s0 = 0; s0 < passes; s0 += every) {
+        int k = (passes - s0) < every ? (passes - s0) : every;
+        const int s = (int)first + s0;
         pmc_result r;
         if (graph) {
             pmc_stats a, b;
@@ -82,7 +98,9 @@ int main(int argc, char** argv) {
             total.de_fixed += r.stats.de_fixed;
         }
         printf("%d: %f\n", s + k, e);
+        if (dump && (rc = pmc_dump_frame(ctx, dump, 1, (int64_t)(s + k)))) die("pmc_dump_frame", rc);
     }
+    if (save && (rc = pmc_save_snapshot(ctx, save, first + (uint32_t)passes))) die("pmc_save_snapshot", rc);
     printf("# acceptance %.6f (accepted %lld / trials %lld, energy-evaluated %lld)\n",
            total.trials ? (double)total.accepted / (double)total.trials : 0.0, (long long)total.accepted,
            (long long)total.trials, (long long)total.evaluated);

@@ -119,6 +119,18 @@ def lib():
         _sig(L, "pmc_plane_span", i32, _vp, i32, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t),
              C.POINTER(C.c_size_t), C.POINTER(C.c_size_t))
         _sig(L, "pmc_selftest_detmath", i32, _vp, i32, _vp, _vp)
+        # trajectory dump / restart (host formats need no GPU)
+        cp, f3 = C.c_char_p, C.POINTER(C.c_float * 3)
+        _sig(L, "pmc_disk_to_r", i32, _vp, _vp, i64, i32, _vp, i64, C.POINTER(i64))
+        _sig(L, "pmc_write_dump", i32, cp, i32, i64, _vp, i64, i64, f3, f3)
+        _sig(L, "pmc_read_dump", i32, cp, i64, C.POINTER(i64), _vp, i64, C.POINTER(i64), f3, f3)
+        _sig(L, "pmc_snapshot_write", i32, cp, P, u32, C.POINTER(Stats), _vp, _vp, i64)
+        _sig(L, "pmc_snapshot_read", i32, cp, P, C.POINTER(u32), C.POINTER(Stats), _vp, _vp, i64)
+        _sig(L, "pmc_get_params", i32, _vp, P)
+        _sig(L, "pmc_stats_write", i32, _vp, C.POINTER(Stats))
+        _sig(L, "pmc_dump_frame", i32, _vp, cp, i32, i64)
+        _sig(L, "pmc_save_snapshot", i32, _vp, cp, u32)
+        _sig(L, "pmc_load_snapshot", i32, _vp, cp, C.POINTER(u32))
         _lib = L
     return _lib
 

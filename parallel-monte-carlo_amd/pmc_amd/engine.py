@@ -193,6 +193,30 @@ class PmcContext:
         assert disk.size == self.cells * 3 * self.nmax and n.size == self.cells
         check("pmc_copy_in", lib().pmc_copy_in(self._h, disk.ctypes.data, n.ctypes.data))
 
+    # ---- trajectory dump / restart (kernel.cu:497-536; pmc_amd.io for the host formats) ----
+    def get_params(self) -> Params:
+        p = Params()
+        check("pmc_get_params", lib().pmc_get_params(self._h, C.byref(p)))
+        return p
+
+    def set_stats(self, stats: dict) -> None:
+        s = Stats(**{k: int(v) for k, v in stats.items()})
+        check("pmc_stats_write", lib().pmc_stats_write(self._h, C.byref(s)))
+
+    def dump_frame(self, path: str, timestep: int, append: bool = True) -> None:
+        """Append (or write) the current state as one create_dump frame (kernel.cu:510-536)."""
+        check("pmc_dump_frame", lib().pmc_dump_frame(self._h, str(path).encode(), int(append), timestep))
+
+    def save_snapshot(self, path: str, next_sweep: int) -> None:
+        """Binary snapshot: parameters, next sweep index (the RNG state), stats, exact coordinates."""
+        check("pmc_save_snapshot", lib().pmc_save_snapshot(self._h, str(path).encode(), next_sweep))
+
+    def load_snapshot(self, path: str) -> int:
+        """Restore a snapshot written by save_snapshot; returns the sweep index to continue from."""
+        sw = C.c_uint32()
+        check("pmc_load_snapshot", lib().pmc_load_snapshot(self._h, str(path).encode(), C.byref(sw)))
+        return sw.value
+
     def plane_span(self, z_local: int):
         a, b, c, d = C.c_size_t(), C.c_size_t(), C.c_size_t(), C.c_size_t()
         check("pmc_plane_span", lib().pmc_plane_span(self._h, z_local, C.byref(a), C.byref(b), C.byref(c),

@@ -13,6 +13,8 @@ Stored vectors (data only; no reference source is copied):
                      (rc = 2.5), 4(r^-12 - r^-6), evaluated here in float64
   max_occupancy[k]   largest cell count of the frame binned into the 4^3 grid (w = 2.5) with the
                      reference's assign rule lb < x <= ub (start.cu:129-134)
+  frame_text_0/1     the exact bytes of frames 0 and 1 as create_dump printed them (uint8) -- the
+                     golden output of the dump writer (pmc_write_dump) and the reader's input
 
 Run:  python tests/golden/make_golden.py
 """
@@ -67,13 +69,29 @@ def max_occ(pos):
     return max(cnt.values())
 
 
+def frame_texts(path, count):
+    """Raw bytes of the first `count` frames (each starts at an 'ITEM: TIMESTEP' line)."""
+    data = open(path, "rb").read()
+    starts = []
+    pos = 0
+    while len(starts) <= count:
+        i = data.find(b"ITEM: TIMESTEP", pos)
+        if i < 0:
+            break
+        starts.append(i)
+        pos = i + 1
+    return [np.frombuffer(data[starts[k]:starts[k + 1]], np.uint8) for k in range(count)]
+
+
 def main():
     frames = parse_frames(SRC)
+    texts = frame_texts(SRC, 2)
     assert len(frames) == 1000, len(frames)
     pos = np.stack([frames[k] for k in KEEP])
     en = np.array([calc_energy(frames[k]) for k in KEEP])
     occ = np.array([max_occ(frames[k]) for k in KEEP])
-    np.savez_compressed(OUT, frame_ids=np.array(KEEP), positions=pos, energy_calc=en, max_occupancy=occ)
+    np.savez_compressed(OUT, frame_ids=np.array(KEEP), positions=pos, energy_calc=en, max_occupancy=occ,
+                        frame_text_0=texts[0], frame_text_1=texts[1])
     print(OUT, en, occ)
 
 
