@@ -238,6 +238,20 @@ class SlabSimulation:
         self._wait(getattr(self, "_pending", None))
         self._pending = None
 
+    # ---- restart (per-rank PMCSNAP1 files of the owned planes) ----------
+    def save_snapshot(self, path: str, next_sweep: int) -> None:
+        """Write this rank's owned planes, stats and the next sweep index (the RNG state)."""
+        self.finish()
+        self.engine.save_snapshot(path, next_sweep)
+
+    def load_snapshot(self, path: str) -> int:
+        """Restore this rank's planes from save_snapshot's file, refill the halos from the
+        neighbours (collective over the ranks), return the sweep index to continue from."""
+        self.finish()
+        sweep = self.engine.load_snapshot(path)
+        self.exchange_full()
+        return sweep
+
     def run(self, first: int, count: int) -> None:
         for k in range(count):
             self.sweep(first + k)

@@ -37,6 +37,33 @@ class OracleEngine:
         self.cur ^= 1
 
 
+    # restart hooks (the HIP engine's are PmcContext.save_snapshot / load_snapshot)
+    def _owned(self):
+        plane = self.p.cps_x * self.p.cps_y
+        return slice(plane, plane * (1 + self.p.nz_local))
+
+    def save_snapshot(self, path, next_sweep):
+        import pmc_amd.io as io
+        sl = self._owned()
+        nm = self.p.nmax
+        io.write_snapshot(path, self.p, next_sweep, self.stats.as_dict(),
+                          self.d[self.cur][sl.start * 3 * nm:sl.stop * 3 * nm], self.nn[self.cur][sl])
+
+    def load_snapshot(self, path):
+        import pmc_amd.io as io
+        sl = self._owned()
+        nm = self.p.nmax
+        q, sweep, stats, disk, n = io.read_snapshot(path, cells=sl.stop - sl.start)
+        assert (q.z0, q.nz_local, q.seed) == (self.p.z0, self.p.nz_local, self.p.seed)
+        self.d[self.cur][:] = 0
+        self.nn[self.cur][:] = 0
+        self.d[self.cur][sl.start * 3 * nm:sl.stop * 3 * nm] = disk
+        self.nn[self.cur][sl] = n
+        for k, v in stats.items():
+            setattr(self.stats, k, v)
+        return sweep
+
+
 def make_oracle_slab(cps, nz, rank, world, nmax, atoms_per_rank, transport):
     g = SlabGeometry(cps, nz, rank, world, nmax)
     p = pmc_oracle.make_params(cps=cps, cps_z=g.cps_z, nz_local=nz, z0=g.z0, halo=1, nmax=nmax)
@@ -74,5 +101,30 @@ def worker(rank, world, port, cps, nz, nmax, atoms, sweeps, out_q):
         sim.run(0, sweeps)
         d1, n1 = sim.owned()
         out_q.put((rank, init, (d1.numpy().copy(), n1.numpy().copy()), sim.engine.stats.as_dict()))
+    finally:
+        dist.destroy_process_group()
+
+
+def worker_restart(rank, world, port, cps, nz, nmax, atoms, snapdir, out_q):
+    """2 sweeps, per-rank snapshot, 2 more sweeps; then fresh slabs restored from the snapshots
+    run the same 2 sweeps: both final states go back for comparison."""
+    import os
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        path = os.path.join(snapdir, f"rank{rank}.pmcsnap")
+        sim = make_oracle_slab(cps, nz, rank, world, nmax, atoms, TorchP2P(rank, world))
+        sim.run(0, 2)
+        sim.save_snapshot(path, 2)
+        sim.run(2, 2)
+        d1, n1 = sim.owned()
+        straight = (d1.numpy().copy(), n1.numpy().copy(), sim.engine.stats.as_dict())
+        sim2 = make_oracle_slab(cps, nz, rank, world, nmax, 0, TorchP2P(rank, world))
+        first = sim2.load_snapshot(path)
+        sim2.run(first, 2)
+        d2, n2 = sim2.owned()
+        out_q.put((rank, straight, (d2.numpy().copy(), n2.numpy().copy(), sim2.engine.stats.as_dict())))
     finally:
         dist.destroy_process_group()

@@ -72,3 +72,24 @@ def test_start_driver_save_restart(pmc, tmp_path):
     import pmc_amd.io as io
     ts, r, _, _ = io.read_dump(dump, 2)          # frames 0, 1, 2
     assert ts == 2 and r.shape == (3, 2000)
+
+
+def test_gpu_slab_snapshot_restart(pmc, oracle, tmp_path):
+    """The RCCL slab driver's restart (one rank: halos are local copies) on the HIP engine."""
+    import torch
+    from pmc_amd.slab import SlabSimulation
+    path = str(tmp_path / "slab.pmcsnap")
+    a = SlabSimulation.create(cps=16, nz_local=16, rank=0, world=1, atoms_per_rank=10_000)
+    a.run(0, 2)
+    a.save_snapshot(path, 2)
+    a.run(2, 2)
+    b = SlabSimulation.create(cps=16, nz_local=16, rank=0, world=1)
+    first = b.load_snapshot(path)
+    b.run(first, 2)
+    torch.cuda.synchronize()
+    da, na = a.owned()
+    db, nb = b.owned()
+    assert torch.equal(na, nb)
+    assert oracle.valid_slots_equal(da.cpu().numpy().reshape(-1), na.cpu().numpy().reshape(-1),
+                                    db.cpu().numpy().reshape(-1), nb.cpu().numpy().reshape(-1), 16)
+    assert a.ctx.stats() == b.ctx.stats()

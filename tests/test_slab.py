@@ -59,3 +59,24 @@ def test_slab_single_rank_periodic(oracle):
     d1, n1 = sim.owned()
     assert np.array_equal(n1.numpy().reshape(-1), st.n)
     assert oracle.valid_slots_equal(d1.numpy().reshape(-1), n1.numpy().reshape(-1), st.disk, st.n, 16)
+
+
+def test_slab_snapshot_restart(oracle, tmp_path):
+    """Per-rank snapshots + halo refill: the restarted 2-rank run equals the uninterrupted one."""
+    world, cps, nz, nmax, atoms = 2, 8, 4, 16, 1000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=slab_helpers.worker_restart, args=(r, world, port, cps, nz, nmax, atoms,
+                                                                   str(tmp_path), q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for _ in range(world):
+        rank, straight, restarted = q.get(timeout=300)
+        assert np.array_equal(straight[1], restarted[1])
+        assert oracle.valid_slots_equal(straight[0].reshape(-1), straight[1].reshape(-1), restarted[0].reshape(-1),
+                                        restarted[1].reshape(-1), nmax)
+        assert straight[2] == restarted[2]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
