@@ -115,10 +115,14 @@ template <> struct DiskAddr<true> {
     __device__ static __forceinline__ float ld(const float* b, uint32_t off) {
         return *(const float*)((const char*)b + (uint64_t)off);
     }
+    __device__ static __forceinline__ void st(float* b, uint32_t off, float v) {
+        *(float*)((char*)b + (uint64_t)off) = v;
+    }
 };
 template <> struct DiskAddr<false> {
     static constexpr uint32_t kUnit = 1;   // offsets in floats
     __device__ static __forceinline__ float ld(const float* b, uint32_t off) { return b[(uint64_t)off]; }
+    __device__ static __forceinline__ void st(float* b, uint32_t off, float v) { b[(uint64_t)off] = v; }
 };
 
 // Philox4x32-10 with the host-computed key schedule (bit-identical to pmc_philox4x32_10: round
@@ -213,16 +217,26 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     const int dx = (int)bit_of(kStencilPos[0], lane) - (int)bit_of(kStencilNeg[0], lane);
     const int dy = (int)bit_of(kStencilPos[1], lane) - (int)bit_of(kStencilNeg[1], lane);
     const int dz = (int)bit_of(kStencilPos[2], lane) - (int)bit_of(kStencilNeg[2], lane);
-    // periodic wrap as selects (no exec-mask branches)
-    const int nx0 = x + dx, ny0 = y + dy, zgn = zg0 + dz;
-    const int nx = nx0 + (nx0 < 0 ? g.cps_x : 0) - (nx0 >= g.cps_x ? g.cps_x : 0);
-    const int ny = ny0 + (ny0 < 0 ? g.cps_y : 0) - (ny0 >= g.cps_y ? g.cps_y : 0);
-    const float k_sx = nx0 < 0 ? -g.Lx : (nx0 >= g.cps_x ? g.Lx : 0.0f);
-    const float k_sy = ny0 < 0 ? -g.Ly : (ny0 >= g.cps_y ? g.Ly : 0.0f);
-    const float k_sz = zgn < 0 ? -g.Lz : (zgn >= g.cps_z ? g.Lz : 0.0f);
-    const int nz0 = zl + dz;
-    const int nzl = g.halo ? nz0 : nz0 + (nz0 < 0 ? g.cps_z : 0) - (nz0 >= g.cps_z ? g.cps_z : 0);
-    const uint32_t kc = (uint32_t)(nx + g.cps_x * ny + plane * (nzl + g.halo));
+    // periodic images only matter for cells on the box faces (apply_PBC, subsweep.h:139-151):
+    // interior waves (~95% at 128^3) take the plain offsets, face waves the wrapped ones
+    const bool edge = x == 0 || x == g.cps_x - 1 || y == 0 || y == g.cps_y - 1 || zg0 == 0 ||
+                      zg0 == g.cps_z - 1;
+    uint32_t kc;
+    float k_sx = 0.0f, k_sy = 0.0f, k_sz = 0.0f;
+    if (!edge) {
+        kc = c + (uint32_t)(dx + g.cps_x * dy + plane * dz);   // (storage is contiguous across halos)
+    } else {
+        // periodic wrap as selects (no exec-mask branches)
+        const int nx0 = x + dx, ny0 = y + dy, zgn = zg0 + dz;
+        const int nx = nx0 + (nx0 < 0 ? g.cps_x : 0) - (nx0 >= g.cps_x ? g.cps_x : 0);
+        const int ny = ny0 + (ny0 < 0 ? g.cps_y : 0) - (ny0 >= g.cps_y ? g.cps_y : 0);
+        k_sx = nx0 < 0 ? -g.Lx : (nx0 >= g.cps_x ? g.Lx : 0.0f);
+        k_sy = ny0 < 0 ? -g.Ly : (ny0 >= g.cps_y ? g.Ly : 0.0f);
+        k_sz = zgn < 0 ? -g.Lz : (zgn >= g.cps_z ? g.Lz : 0.0f);
+        const int nz0 = zl + dz;
+        const int nzl = g.halo ? nz0 : nz0 + (nz0 < 0 ? g.cps_z : 0) - (nz0 >= g.cps_z ? g.cps_z : 0);
+        kc = (uint32_t)(nx + g.cps_x * ny + plane * (nzl + g.halo));
+    }
     const int k_cnt = ncnt[kc];
     const uint32_t k_off = kc * row * DiskAddr<OFF32>::kUnit;   // bytes (OFF32) or floats
     const int p = lane & (NSLOT - 1);
@@ -315,11 +329,8 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     float blo[3], bhi[3];
     pmc_cell_box(x, y, zg0, g.w, g.Lx, g.Ly, g.Lz, blo, bhi);
     int S_nb = 0;
-    // periodic images only matter for cells on the box faces (apply_PBC, subsweep.h:139-151):
     // interior waves skip the image adds (an add of +0 changes nothing downstream -- staged
     // coordinates only enter differences that are squared)
-    const bool edge = x == 0 || x == g.cps_x - 1 || y == 0 || y == g.cps_y - 1 || zg0 == 0 ||
-                      zg0 == g.cps_z - 1;
     auto stage = [&](auto with_image) {
 #pragma unroll
         for (int q = 0; q < NP; ++q) {
@@ -465,14 +476,17 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     PMC_STAMP(8);
     // ---- 5. write back the own cell in shuffled order (cpy_D_sh_to_Disk, subsweep.h:29-36) ----
     if (lane < n_own) {
-        const uint32_t off = c * (uint32_t)(3 * nm) + (uint32_t)lane;
-        disk[off] = px_[S_nb + lane];
-        disk[off + nm] = py_[S_nb + lane];
-        disk[off + 2 * nm] = pz_[S_nb + lane];
+        using A = DiskAddr<OFF32>;
+        const uint32_t off = (c * (uint32_t)(3 * nm) + (uint32_t)lane) * A::kUnit;
+        A::st(disk, off, px_[S_nb + lane]);
+        A::st(disk, off + (uint32_t)nm * A::kUnit, py_[S_nb + lane]);
+        A::st(disk, off + 2u * (uint32_t)nm * A::kUnit, pz_[S_nb + lane]);
     }
+    // fixed-point conversion only when something was accepted (pmc_to_fixed(0) == 0)
+    const int64_t de_fix = n_acc ? pmc_to_fixed(de_cell) : 0;
     if (lane == 0) {
         const int slot = t & (kStatSlots - 1);
-        atomicAdd(&stats[0 * kStatSlots + slot], (unsigned long long)pmc_to_fixed(de_cell));
+        atomicAdd(&stats[0 * kStatSlots + slot], (unsigned long long)de_fix);
         atomicAdd(&stats[1 * kStatSlots + slot], (unsigned long long)n_acc);
         atomicAdd(&stats[2 * kStatSlots + slot], (unsigned long long)g.n_moves);
         atomicAdd(&stats[3 * kStatSlots + slot], (unsigned long long)n_ev);
