@@ -225,6 +225,15 @@ PMC_HD float pmc_box_d2(float x, float y, float z, const float lo[3], const floa
     return pmc_r2(tx, ty, tz);
 }
 
+/* Staging order of the neighbour partners (spec, kernels and oracle): in stencil order, first
+ * slots [0, H) of every neighbour cell, then slots [H, n) of the cells holding more than H, with
+ * H = nslot/2 for nslot >= 16 else nslot (nslot = smallest power of two >= max(nmax, 8)). */
+PMC_HD int pmc_stage_split(int nmax) {
+    int nslot = 8;
+    while (nslot < nmax) nslot <<= 1;
+    return nslot >= 16 ? nslot / 2 : nslot;
+}
+
 /* own-cell closed box padded by PMC_BOX_PAD: lb = c*w - L/2.0f (start.cu:129), ub = lb + w */
 PMC_HD void pmc_cell_box(int cx, int cy, int cz, float w, float Lx, float Ly, float Lz, float lo[3],
                          float hi[3]) {

@@ -192,16 +192,23 @@ static void subsweep_cell(const pmc_params* p, float* disk, const int16_t* n, in
     pmc_cell_box(x, y, p->z0 + zl, p->w, Lx, Ly, Lz, lo, hi);
     const float rcf = pmc_filter_r2(rc2);
     int S = 0;
-    for (int k = 1; k < 27; ++k) {
-        nbref b = nb_of(p, x, y, zl, off[k][0], off[k][1], off[k][2]);
-        int cnt = n[b.idx];
-        for (int q = 0; q < cnt; ++q) {
-            float vx = disk[b.idx * 3 * nm + q] + b.sx;
-            float vy = disk[b.idx * 3 * nm + nm + q] + b.sy;
-            float vz = disk[b.idx * 3 * nm + 2 * nm + q] + b.sz;
-            if (pmc_box_d2(vx, vy, vz, lo, hi) <= rcf) {
-                px_[S] = vx; py_[S] = vy; pz_[S] = vz;
-                ++S;
+    /* staging order (pmc_stage_split): slots [0, H) of every neighbour in stencil order, then
+     * slots [H, n) of the neighbours holding more than H particles, in stencil order */
+    const int H = pmc_stage_split(nm);
+    for (int round = 0; round < 2; ++round) {
+        for (int k = 1; k < 27; ++k) {
+            nbref b = nb_of(p, x, y, zl, off[k][0], off[k][1], off[k][2]);
+            int cnt = n[b.idx];
+            const int q0 = round ? H : 0;
+            const int q1 = round ? cnt : (cnt < H ? cnt : H);
+            for (int q = q0; q < q1; ++q) {
+                float vx = disk[b.idx * 3 * nm + q] + b.sx;
+                float vy = disk[b.idx * 3 * nm + nm + q] + b.sy;
+                float vz = disk[b.idx * 3 * nm + 2 * nm + q] + b.sz;
+                if (pmc_box_d2(vx, vy, vz, lo, hi) <= rcf) {
+                    px_[S] = vx; py_[S] = vy; pz_[S] = vz;
+                    ++S;
+                }
             }
         }
     }

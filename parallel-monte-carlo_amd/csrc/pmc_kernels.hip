@@ -97,6 +97,13 @@ constexpr uint32_t stencil_mask(int axis, int h) {
 __device__ constexpr uint32_t kStencilNeg[3] = {stencil_mask(0, 1), stencil_mask(1, 1), stencil_mask(2, 1)};
 __device__ constexpr uint32_t kStencilPos[3] = {stencil_mask(0, 2), stencil_mask(1, 2), stencil_mask(2, 2)};
 
+// Staging lanes per stencil cell: slots [0, HS) of every neighbour are staged in the main passes
+// (loaded with the visit's single HBM round trip); slots [HS, nmax) -- only cells holding more than
+// HS particles, ~1.6% of cells at 4.77 per cell -- in overflow passes.  Half the lanes per cell of
+// the full row for nmax >= 16: 4 main passes instead of 7 at nmax = 16.  The staged order (all
+// cells' low slots, then the overflow cells' high slots) is part of the spec the oracle follows.
+__host__ __device__ constexpr int stage_split(int nslot) { return nslot >= 16 ? nslot / 2 : nslot; }
+
 // lanes of staging pass q whose stencil cell k = 1 + q*CPP + lane/NSLOT is < 27
 template <int NSLOT>
 __device__ constexpr unsigned long long stage_lane_mask(int q) {
@@ -189,8 +196,9 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
                                               uint32_t sweep, unsigned long long* __restrict__ stats,
                                               float* __restrict__ px_, int lcap_rt, int cap, int t,
                                               int cz0) {
-    constexpr int CPP = kWave / NSLOT;            // stencil cells staged per pass
-    constexpr int NP = (26 + CPP - 1) / CPP;      // staging passes over the 26 neighbours
+    constexpr int HS = stage_split(NSLOT);        // staging lanes per stencil cell (main passes)
+    constexpr int CPP = kWave / HS;               // stencil cells staged per pass
+    constexpr int NP = (26 + CPP - 1) / CPP;      // main staging passes over the 26 neighbours
     const int lane = threadIdx.x & (kWave - 1);
     const int nm = NMC > 0 ? NMC : g.nmax;        // compile-time for the common nmax
     const int lcap = LCAP > 0 ? LCAP : lcap_rt;            // layout capacity (>= cap)
@@ -239,8 +247,8 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     }
     const int k_cnt = ncnt[kc];
     const uint32_t k_off = kc * row * DiskAddr<OFF32>::kUnit;   // bytes (OFF32) or floats
-    const int p = lane & (NSLOT - 1);
-    const int kk = lane / NSLOT;
+    const int p = lane & (HS - 1);
+    const int kk = lane / HS;
     const int pp = p < nm ? p : 0;
     const uint32_t pp_off = (uint32_t)pp * DiskAddr<OFF32>::kUnit;
     const uint32_t nm_off = (uint32_t)nm * DiskAddr<OFF32>::kUnit;
@@ -331,6 +339,20 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     int S_nb = 0;
     // interior waves skip the image adds (an add of +0 changes nothing downstream -- staged
     // coordinates only enter differences that are squared)
+    // append the lanes of `valid` whose partner passes the box filter, in lane order
+    auto append = [&](float ux, float uy, float uz, unsigned long long valid) {
+        const unsigned long long mk = __builtin_amdgcn_ballot_w64(pmc_box_d2(ux, uy, uz, blo, bhi) <= g.rc2f) & valid;
+        const int nk = wave_uniform(__popcll(mk));
+        if (S_nb + nk <= cap_nb) {            // otherwise the cell goes to the fallback
+            // unconditional stores, discarded lanes into the row tails (>= 32 slots)
+            const int slot = select_by_mask(mk, S_nb + mbcnt64(mk), stride - 32 + (lane & 31));
+            float* dst = px_ + slot;
+            dst[0] = ux;
+            dst[stride] = uy;
+            dst[2 * stride] = uz;
+        }
+        S_nb += nk;
+    };
     auto stage = [&](auto with_image) {
 #pragma unroll
         for (int q = 0; q < NP; ++q) {
@@ -344,19 +366,34 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
                 uz = uz + __shfl(k_sz, ks);
             }
             // lanes of stencil cells k < 27 (compile-time per pass), slot < count, box filter
-            const unsigned long long live = stage_lane_mask<NSLOT>(q);
-            const unsigned long long mk = __builtin_amdgcn_ballot_w64(pmc_box_d2(ux, uy, uz, blo, bhi) <= g.rc2f) &
-                                          __builtin_amdgcn_ballot_w64(p < cnt) & live;
-            const int nk = wave_uniform(__popcll(mk));
-            if (S_nb + nk <= cap_nb) {            // otherwise the cell goes to the fallback
-                // unconditional stores, discarded lanes into the row tails (>= 32 slots)
-                const int slot = select_by_mask(mk, S_nb + mbcnt64(mk), stride - 32 + (lane & 31));
-                float* dst = px_ + slot;
-                dst[0] = ux;
-                dst[stride] = uy;
-                dst[2 * stride] = uz;
+            const unsigned long long live = stage_lane_mask<HS>(q);
+            append(ux, uy, uz, __builtin_amdgcn_ballot_w64(p < cnt) & live);
+        }
+        if constexpr (HS < NSLOT) {
+            // overflow passes: slots [HS, nmax) of the neighbours holding more than HS particles,
+            // in stencil order, CPP cells per pass (lane group j: the j-th remaining cell); loads
+            // issued here (the rare case pays its own round trip)
+            unsigned long long ovm = __builtin_amdgcn_ballot_w64(lane >= 1 && lane < 27 && k_cnt > HS);
+            while (ovm) {
+                int ks = 26, ncell = 0;
+                for (; ncell < CPP && ovm; ++ncell) {
+                    const int kb = (int)__builtin_ctzll(ovm);
+                    ovm &= ovm - 1ull;
+                    ks = kk == ncell ? kb : ks;
+                }
+                const int cnt = __shfl(k_cnt, ks);
+                const int ps = HS + p;                                    // slot in the row
+                const uint32_t off = (uint32_t)__shfl((int)k_off, ks) + (uint32_t)(ps < nm ? ps : 0) * DiskAddr<OFF32>::kUnit;
+                float ux = DiskAddr<OFF32>::ld(disk, off);
+                float uy = DiskAddr<OFF32>::ld(disk, off + nm_off);
+                float uz = DiskAddr<OFF32>::ld(disk, off + 2 * nm_off);
+                if constexpr (decltype(with_image)::value) {
+                    ux = ux + __shfl(k_sx, ks);
+                    uy = uy + __shfl(k_sy, ks);
+                    uz = uz + __shfl(k_sz, ks);
+                }
+                append(ux, uy, uz, __builtin_amdgcn_ballot_w64(kk < ncell && ps < cnt));
             }
-            S_nb += nk;
         }
     };
     if (edge) stage(std::true_type{});
