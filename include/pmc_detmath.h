@@ -116,13 +116,12 @@ PMC_HD void pmc_det_sincos_2pi(float u, float* s_out, float* c_out) {
                + x2 * (2.48015876e-05f + x2 * -2.75573192e-07f))));
     float sr = comp ? cx : sx;       /* sin(r*pi/2) */
     float cr = comp ? sx : cx;       /* cos(r*pi/2) */
-    float so, co;
-    if (q == 0)      { so = sr;  co = cr;  }
-    else if (q == 1) { so = cr;  co = -sr; }
-    else if (q == 2) { so = -sr; co = -cr; }
-    else             { so = -cr; co = sr;  }
-    *s_out = so;
-    *c_out = co;
+    /* quadrant q: (sin, cos) = (sr, cr), (cr, -sr), (-sr, -cr), (-cr, sr) -- as selects and
+     * sign flips (no branches; identical values) */
+    float ua = (q & 1) ? cr : sr;
+    float ub = (q & 1) ? sr : cr;
+    *s_out = (q & 2) ? -ua : ua;
+    *c_out = ((q + 1) & 2) ? -ub : ub;
 }
 
 /* Box-Muller radius sqrt(-2 log u) (sqrtf is correctly rounded on both targets). */

@@ -616,7 +616,7 @@ __global__ __launch_bounds__(256) void k_shift(DevGeom g, const float* __restric
     const uint32_t plane = (uint32_t)g.cps_x * (uint32_t)g.cps_y;
     const int pp = p < nm ? p : 0;
     const int gsh = lane & ~(NSLOT - 1);
-    const unsigned long long gmask = NSLOT == 64 ? ~0ull : ((1ull << NSLOT) - 1ull);
+    const unsigned long long gmask = NSLOT == 64 ? ~0ull : ((1ull << (NSLOT & 63)) - 1ull);
     const unsigned long long below = (1ull << p) - 1ull;
 
     bool live[U];
