@@ -82,6 +82,19 @@ __device__ __forceinline__ int select_by_mask(unsigned long long m, int a, int b
     return __builtin_amdgcn_inverse_ballot_w64(m) ? a : b;
 }
 
+// pmc_lj4_signed_m with the r2 floor as ONE v_max_f32 (|r2s| is a free source modifier; the
+// compiler's fmaxf would add canonicalizing maxes, the C form a compare + select): identical
+// values for the non-NaN inputs of the term list (max(|r2s|, r2min) == (|r2s| < r2min ? r2min :
+// |r2s|)).
+__device__ __forceinline__ float lj4_signed_max(float r2s, float r2min) {
+    float rr;
+    asm("v_max_f32_e64 %0, |%1|, %2" : "=v"(rr) : "v"(r2s), "s"(r2min));
+    const float inv = pmc_recip(rr);
+    const float invs = __builtin_copysignf(inv, r2s);
+    const float p6s = (inv * inv) * invs;
+    return p6s * __builtin_fabsf(p6s) - p6s;
+}
+
 __device__ __forceinline__ uint32_t bit_of(uint32_t m, int lane) { return (m >> (lane & 31)) & 1u; }
 
 // Stencil lane masks: lane k = 9*hx + 3*hy + hz < 27; Neg[a] has the lanes whose offset along
@@ -416,6 +429,7 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     // (+inf -> r2 = inf, never listed).  roundup64(K) <= stride; the clamp keeps every lane's
     // store inside the x row.
     const float kFar = __builtin_inff();
+    const float kPad = 1.0e30f;
     px_[(K + lane) < stride ? K + lane : stride - 1] = kFar;
 
     PMC_STAMP(7);
@@ -484,13 +498,12 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
                     block(kWave);
                     for (int base = 2 * kWave; base < K; base += kWave) block(base);
                 }
-                // 4b. energies of the listed terms: term t on lane t % 64, ascending t
+                // 4b. energies of the listed terms: term t on lane t % 64, ascending t.  The 64
+                // slots after the list get kPad (r2 = 1e30: inv^3 underflows to +0, so the term
+                // is exactly +0 and adding it leaves a lane's sum unchanged) -- no lane mask.
+                buf[C + lane] = kPad;
                 float acc = 0.0f;
-                for (int t0 = 0; t0 < C; t0 += kWave) {
-                    const int tt = t0 + lane;
-                    const float us = pmc_lj4_signed_m(buf[tt], r2min);   // buf padded: no clamp
-                    acc = acc + (tt < C ? us : 0.0f);
-                }
+                for (int t0 = 0; t0 < C; t0 += kWave) acc = acc + lj4_signed_max(buf[t0 + lane], r2min);
                 // quarter energies were accumulated; the factor 4 is exact, so 4*(sum of u)
                 // equals the sum of the 4u the oracle accumulates, bit for bit
                 const float dE = wave_sum_fixed_order(4.0f * acc);
