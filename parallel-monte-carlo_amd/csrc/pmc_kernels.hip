@@ -197,8 +197,8 @@ __device__ __forceinline__ int64_t sidx(const DevGeom& g, int x, int y, int zl) 
 //      DPP/permlane reduction gives dE; accept in-kernel, wave-uniformly;
 //   5. write back the own cell; one atomic per counter per wave.
 // LDS per wave (capacity lcap): x, y, z rows of `stride` = subsweep_stride(lcap) slots, then the
-// term list (2 * lcap + 64 floats; the extra 64 are per-lane discard slots and let a pass read a
-// full 64-lane block without clamping).  Row slots past the last partner hold +inf ("far"), as
+// term list (2 * lcap + 64 floats; the extra 64 hold the kPad entries after the list, so a pass
+// reads a full 64-lane block without a lane mask).  Row slots past the last partner hold +inf ("far"), as
 // does the moving particle's own slot during its move, so no lane mask is needed in the moves.
 // ------------------------------------------------------------------------------------------
 // Returns false (and leaves the cell untouched) when the cell's staged partners do not fit the
@@ -474,10 +474,6 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
                 // ~80% of staged pairs lie beyond rc for a given position; they are exactly 0
                 // and never reach the reciprocal.
                 int C = 0;   // wave-uniform
-                // Stores are unconditional: a lane whose term is not listed writes to its own
-                // discard slot 2*lcap + lane past the list (one v_cndmask instead of exec-mask save/restore, which
-                // would cost scalar instructions -- the CU's single scalar unit is the busier
-                // issue port in this loop).
                 auto block = [&](int base) {
                     // slots >= K and the moving slot hold +inf in x: their r2 is inf, never listed
                     const int k = base + lane;
@@ -489,8 +485,10 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
                     const unsigned long long mn = __builtin_amdgcn_ballot_w64(r2n <= rc2);
                     const unsigned long long mo = __builtin_amdgcn_ballot_w64(r2on >= nrc2);
                     const int cn = C + __popcll(mn);
-                    buf[select_by_mask(mn, mbcnt64_add(mn, C), 2 * lcap + lane)] = r2n;
-                    buf[select_by_mask(mo, mbcnt64_add(mo, cn), 2 * lcap + lane)] = r2on;
+                    // exec-masked stores (2 SALU each) beat a select into a discard slot (one
+                    // half-rate v_cndmask per list on gfx950)
+                    if (__builtin_amdgcn_inverse_ballot_w64(mn)) buf[mbcnt64_add(mn, C)] = r2n;
+                    if (__builtin_amdgcn_inverse_ballot_w64(mo)) buf[mbcnt64_add(mo, cn)] = r2on;
                     C = cn + __popcll(mo);
                 };
                 block(0);
