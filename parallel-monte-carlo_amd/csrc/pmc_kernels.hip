@@ -356,10 +356,9 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     auto append = [&](float ux, float uy, float uz, unsigned long long valid) {
         const unsigned long long mk = __builtin_amdgcn_ballot_w64(pmc_box_d2(ux, uy, uz, blo, bhi) <= g.rc2f) & valid;
         const int nk = wave_uniform(__popcll(mk));
-        if (S_nb + nk <= cap_nb) {            // otherwise the cell goes to the fallback
-            // unconditional stores, discarded lanes into the row tails (>= 32 slots)
-            const int slot = select_by_mask(mk, S_nb + mbcnt64(mk), stride - 32 + (lane & 31));
-            float* dst = px_ + slot;
+        // otherwise the cell goes to the fallback; exec-masked stores of the kept lanes
+        if (S_nb + nk <= cap_nb && __builtin_amdgcn_inverse_ballot_w64(mk)) {
+            float* dst = px_ + S_nb + mbcnt64(mk);
             dst[0] = ux;
             dst[stride] = uy;
             dst[2 * stride] = uz;
