@@ -97,6 +97,31 @@ def test_shift_parity(pmc, oracle, f, d):
     assert int(got_n.sum()) == 10_000
 
 
+@pytest.mark.parametrize("cps,atoms", [(6, 600), (12, 5000), (20, 30000)])
+@pytest.mark.parametrize("f,d", [(0, 0.9), (1, -0.6), (2, 1.1), (2, -1.2)])
+def test_shift_sizes_parity(pmc, oracle, cps, atoms, f, d):
+    """shiftCells at other box sizes (6, 12, 20 cells per side) along every axis, both directions."""
+    ctx = _ctx(pmc, cps)
+    ctx.init_lattice(atoms)
+    ctx.start(0, 1)
+    disk, n = ctx.copy_out()
+    st = _ostate(oracle, cps)
+    st.disk[:] = disk
+    st.n[:] = n
+    import torch
+    dev = torch.device("cuda")
+    din = torch.from_numpy(disk).to(dev)
+    nin = torch.from_numpy(n).to(dev)
+    dout = torch.zeros_like(din)
+    nout = torch.zeros_like(nin)
+    ctx.shiftCells(din, nin, dout, nout, f, d)
+    ctx.synchronize()
+    assert st.shift_cells(f, d) == 0
+    got_d, got_n = dout.cpu().numpy(), nout.cpu().numpy()
+    assert np.array_equal(got_n, st.n)
+    assert oracle.valid_slots_equal(got_d, got_n, st.disk, st.n, 16)
+
+
 def test_full_sweeps_parity_16(pmc, oracle):
     ctx = _ctx(pmc, 16)
     ctx.init_lattice(10_000)
