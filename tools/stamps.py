@@ -2,8 +2,9 @@
 
   PMC_LIB_PATH=.../lib_stamps.so python tools/stamps.py
 
-Stamps per cell visit (main launch): 0 entry, 1 loads issued, 2 RNG done, 3 own count known,
-4 shuffle done, 5 staging done, 6 moves done, 7 written back.
+Stamps per cell visit (main launch): 0 entry, 1 stencil table + count load issued, 2 row loads
+issued, 3 RNG done, 4 own count known, 5 shuffle done, 6 neighbours staged, 7 own cell staged,
+8 moves done, 9 written back.
 """
 import ctypes as C
 import os
@@ -28,21 +29,22 @@ L = pmc_amd._lib.lib()
 L.pmc_debug_stamps.restype = C.c_int
 L.pmc_debug_stamps.argtypes = [C.c_size_t, C.c_void_p]
 ncell = (cps // 2) ** 3
-names = ["stencil+loads", "rng", "count wait", "shuffle", "staging", "moves", "writeback"]
+names = ["stencil+cnt", "row loads", "rng", "count wait", "shuffle", "staging", "own stage", "moves", "writeback"]
 for rep in range(2):
     assert L.pmc_debug_stamps(ncell, None) == 0
     t0 = time.perf_counter()
     ctx.phase(rep, 100 + rep)
     ctx.synchronize()
     dt = time.perf_counter() - t0
-    st = np.zeros((ncell, 8), np.uint64)
-    assert L.pmc_debug_stamps(ncell, st.ctypes.data) == 0
+    raw = np.zeros((ncell, 16), np.uint64)
+    assert L.pmc_debug_stamps(ncell, raw.ctypes.data) == 0
+    st = raw[:, :10].copy()
     full = np.all(st > 0, axis=1)
     s = st[full].astype(np.int64)
     base = int(st[st[:, 0] > 0, 0].min())
-    span = int(st[full, 7].max()) - base
+    span = int(st[full, 9].max()) - base
     d = np.diff(s, axis=1)
-    life = s[:, 7] - s[:, 0]
+    life = s[:, 9] - s[:, 0]
     print(f"phase {rep}: wall {dt*1e3:.3f} ms, stamp span {span} ticks -> {span/dt/1e6:.0f} MHz-equiv; "
           f"visits {full.sum()} of {ncell}")
     for k, nm in enumerate(names):
@@ -51,5 +53,5 @@ for rep in range(2):
     print(f"  lifetime mean {life.mean():.0f} median {np.median(life):.0f} p99 {np.percentile(life, 99):.0f}")
     starts = np.sort(st[full, 0].astype(np.int64) - base)
     print(f"  start quantiles (ticks): " + " ".join(f"{q}%:{np.percentile(starts, q):.0f}" for q in (1, 10, 50, 90, 99)))
-    ends = np.sort(st[full, 7].astype(np.int64) - base)
+    ends = np.sort(st[full, 9].astype(np.int64) - base)
     print(f"  end quantiles (ticks):   " + " ".join(f"{q}%:{np.percentile(ends, q):.0f}" for q in (1, 10, 50, 90, 99, 100)))
