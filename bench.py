@@ -8,6 +8,8 @@ config 3 (128^3 cells, 1e7 particles per GPU, w=rc=2.5, beta=0.3, sigma=0.5, n_M
 Philox seed 1234, reference lattice start) with the state resident in HBM.  With N>1 ranks every
 rank owns a 128^3-cell slab of a 128x128x(128N) periodic box (weak scaling; the 8-rank point has
 the per-GPU work of config 5) and exchanges halo planes with its z-neighbours over RCCL.
+--strong runs BASELINE config 4 instead: ONE 128^3 box with 1e7 particles split into N slabs of
+128/N planes (the 1-GPU state, plane for plane), "scaling": "strong".
 
 Rank 0 prints ONE JSON line with value = trial moves per second over all ranks, the roofline of
 the dominant kernel (subsweep; algorithmic bytes per launch / HIP-event launch time vs 8 TB/s)
@@ -64,7 +66,34 @@ def cpu_baseline(disk: np.ndarray, n: np.ndarray, cps: int, sweeps: int, threads
     trials = st.stats.trials
     return {"value": trials / dt, "unit": "trial-moves/s", "cores": threads, "kind": "port",
             "sample": f"{sweeps} full sweep(s) of the {cps}^3-cell box from the GPU state "
-                      f"(C oracle, OpenMP over cells of a colour, {threads} threads), {dt:.2f} s"}
+                      f"(C oracle, OpenMP over cells of a colour, {threads} threads), {dt:.2f} s"}, st
+
+
+def parity_leg(sim, one_sweep, disk0, n0, sweep0: int, sweeps: int, e0: float, ost) -> dict:
+    """The metric's "+ mean-energy error vs reference": rerun the CPU sample's sweeps on the GPU
+    from the same state (disk0/n0 at sweep index sweep0) and compare with the oracle's result:
+    energy (GPU cell-list energy vs oracle energy), acceptance ratio, and every occupied slot."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pmc_oracle  # test infrastructure: the checker, never the measured path
+    sim.copy_in(disk0, n0)
+    sim.stats(reset=True)
+    for k in range(sweeps):
+        one_sweep(sweep0 + k, False)
+    sim.synchronize()
+    g = sim.stats()
+    e_gpu = sim.energy()
+    disk_g, n_g = sim.copy_out()
+    c = ost.stats.as_dict()
+    e_cpu = ost.energy()
+    same = bool(np.array_equal(n_g, ost.n)) and pmc_oracle.valid_slots_equal(disk_g, n_g, ost.disk, ost.n, ost.nmax)
+    acc_g = g["accepted"] / g["trials"] if g["trials"] else 0.0
+    acc_c = c["accepted"] / c["trials"] if c["trials"] else 0.0
+    rel = lambda a, b: abs(a - b) / abs(b) if b else abs(a - b)
+    return {"reference": "C oracle (corrected-mode restatement of subsweep.h / shiftCells.h)",
+            "sweeps": sweeps, "first_sweep": sweep0, "energy_start": e0,
+            "energy_gpu": e_gpu, "energy_cpu": e_cpu, "energy_rel_err": rel(e_gpu, e_cpu),
+            "acceptance_gpu": acc_g, "acceptance_cpu": acc_c, "acceptance_rel_err": rel(acc_g, acc_c),
+            "counters_equal": g == c, "state_bitwise_equal": same}
 
 
 def traffic_from_profile() -> dict | None:
@@ -90,6 +119,9 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--graph", action="store_true", help="replay the timed sweeps as one hipGraph")
     ap.add_argument("--slab", action="store_true", help="use the z-slab/halo path even with one rank")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling (BASELINE config 4): one cps^3 box of --atoms particles split into "
+                         "world z-slabs of cps/world planes (default: weak, cps^3 and --atoms per GPU)")
     args = ap.parse_args()
 
     import torch
@@ -113,6 +145,12 @@ def main() -> int:
             dist.barrier()
 
     slab = world > 1 or args.slab
+    nz_local = cps // world if args.strong else cps
+    # weak: a lattice of --atoms per cps^3 of slab; strong: ONE lattice of --atoms over the whole
+    # box, each rank keeping its planes (the 1-GPU config 3 state, split)
+    atoms_local = args.atoms * nz_local // cps
+    if slab and (nz_local % 2 or nz_local < 2):
+        raise SystemExit(f"slab thickness {nz_local} must be even and >= 2")
     events = []      # (kind, start, end) HIP events on the kernels' stream
 
     def timer(kind, fn, record):
@@ -143,15 +181,16 @@ def main() -> int:
         cps_z = cps
     else:
         from pmc_amd.slab import SlabSimulation
-        sim_s = SlabSimulation.create(cps=cps, nz_local=cps, rank=rank, world=world, stream=stream,
-                                      atoms_per_rank=args.atoms)
+        sim_s = SlabSimulation.create(cps=cps, nz_local=nz_local, rank=rank, world=world, stream=stream,
+                                      atoms_per_rank=0 if args.strong else atoms_local,
+                                      atoms_total=args.atoms if args.strong else 0)
         sim = sim_s.ctx
 
         def one_sweep(s, record):
             sim_s.sweep(s, timer=lambda kind, fn: timer(kind, fn, record))
 
         finish = sim_s.finish
-        cps_z = cps * world
+        cps_z = nz_local * world
 
     # warmup
     for s in range(args.warmup):
@@ -163,20 +202,22 @@ def main() -> int:
     disk_h, n_h = sim.copy_out()
     plane = cps * cps
     lo = plane if slab else 0
-    n_owned = n_h[lo:lo + plane * cps].astype(np.int64)
+    nzl = nz_local if slab else cps
+    n_owned = n_h[lo:lo + plane * nzl].astype(np.int64)
     if not slab:
         stencil = stencil_counts(n_owned, (cps, cps, cps))
     else:
-        ext = n_h.astype(np.int64).reshape(cps + 2, cps, cps)
+        ext = n_h.astype(np.int64).reshape(nzl + 2, cps, cps)
         g = ext
-        s = np.zeros((cps, cps, cps), np.int64)
+        s = np.zeros((nzl, cps, cps), np.int64)
         for dz in (-1, 0, 1):
-            sub = g[1 + dz:1 + dz + cps]
+            sub = g[1 + dz:1 + dz + nzl]
             for dy in (-1, 0, 1):
                 for dx in (-1, 0, 1):
                     s += np.roll(sub, shift=(-dy, -dx), axis=(1, 2))
         stencil = s.reshape(-1)
     abytes = algorithmic_bytes_per_sweep(n_owned, stencil)
+    e_start = sim.energy()      # cell-list energy of the state the timed region starts from
 
     barrier()
     torch.cuda.synchronize()
@@ -209,6 +250,14 @@ def main() -> int:
         trials_total = trials_local
     flags = sim.error_flags()
     value = trials_total / elapsed
+    # energy bookkeeping over the timed sweeps: E_start + sum of accepted dE (fixed point 2^-32,
+    # order-independent) against a direct cell-list evaluation of the final state
+    e_end = sim.energy()
+    de_timed = st["de_fixed"] / 2.0 ** 32
+    if world > 1:   # slab energies count boundary pairs half on each side: the sum is the box's
+        ev = torch.tensor([e_start, e_end, de_timed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(ev)
+        e_start, e_end, de_timed = (float(v) for v in ev.tolist())
 
     if rank == 0:
         avg_launch_s = (phase_total_ms / n_phases * 1e-3) if n_phases else None
@@ -222,10 +271,12 @@ def main() -> int:
                 "shift_ms": shift_total_ms / args.steps if n_phases else None,
                 "algorithmic_bytes_per_launch": abytes["subsweep_launch"]}
         cpu = None
+        parity = None
         if not args.no_cpu_baseline and not slab:
             try:
                 thr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-                cpu = cpu_baseline(disk_h, n_h, cps, args.cpu_sweeps, thr, first)
+                cpu, ost = cpu_baseline(disk_h, n_h, cps, args.cpu_sweeps, thr, first)
+                parity = parity_leg(sim, one_sweep, disk_h, n_h, first, args.cpu_sweeps, e_start, ost)
             except Exception as e:  # the baseline is reported, never the measured value
                 cpu = {"error": repr(e)}
         sweeps_per_s = args.steps / elapsed
@@ -238,17 +289,23 @@ def main() -> int:
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (reference simple-cubic lattice start, Philox seed 1234)",
-            "config": {"workload": f"{cps}^3 cells x {args.atoms:.0e} particles per GPU, full checkerboard "
-                                   f"sweep (8 colour phases + shiftCells), box {cps}x{cps}x{cps_z}",
-                       "cells_per_gpu": cps ** 3, "particles_per_gpu": args.atoms, "n_moves": 10,
+            "config": {"workload": (f"{cps}^3 cells x {args.atoms:.0e} particles in total" if args.strong else
+                                    f"{cps}x{cps}x{nzl} cells x {atoms_local:.0e} particles per GPU") +
+                                   f", full checkerboard sweep (8 colour phases + shiftCells), box {cps}x{cps}x{cps_z}",
+                       "cells_per_gpu": cps * cps * nzl, "particles_per_gpu": atoms_local, "n_moves": 10,
                        "nmax": 16, "beta": 0.3, "sigma": 0.5, "w": 2.5,
-                       "parallelism": f"z-slab x{world} (RCCL halo planes)" if slab else "single GPU"},
+                       "parallelism": f"z-slab x{world}, {nzl} planes per rank (RCCL halo planes)" if slab else "single GPU"},
             "sweeps_per_s": sweeps_per_s,
             "acceptance": st["accepted"] / st["trials"] if st["trials"] else None,
+            "energy": {"start": e_start, "end": e_end, "start_plus_sum_dE": e_start + de_timed,
+                       "per_particle_end": e_end / (atoms_local * world),
+                       "bookkeeping_rel_err": abs(e_start + de_timed - e_end) / abs(e_end) if e_end else None,
+                       "particles": atoms_local * world},
+            "parity": parity,
             "error_flags": flags,
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -117,6 +117,12 @@ int pmc_shift_cells(pmc_ctx* ctx, const float* d_disk_in, const int16_t* d_n_in,
 /* ---- driver (start.cu:169-272 main loop, kernel.cu:652-701) ------------------------- */
 /* Initialise the context state from a lattice of n_atoms particles (init_r + assign). */
 int pmc_init_lattice(pmc_ctx* ctx, int64_t n_atoms);
+/* Strong-scaling start state (BASELINE config 4): the lattice of n_atoms_total particles over the
+ * WHOLE periodic box (init_r as for a whole-box context), of which this slab keeps the particles
+ * of its owned planes (assign, start.cu:87-146, restricted to z0 <= cz < z0 + nz_local).  The
+ * owned planes equal the same planes of a whole-box pmc_init_lattice, slot for slot.  With no
+ * slab (z0 = 0, nz_local = cps_z) it is pmc_init_lattice. */
+int pmc_init_lattice_global(pmc_ctx* ctx, int64_t n_atoms_total);
 /* One full MC sweep on the context state: colour order from the sweep plan, 8 subsweeps,
  * shiftCells, buffer swap (start.cu:237-260).  Asynchronous. */
 int pmc_sweep(pmc_ctx* ctx, uint32_t sweep);

@@ -330,6 +330,39 @@ int pmc_init_lattice(pmc_ctx* c, int64_t n_atoms) {
     return pmc_assign(c, c->d_r, n_atoms, c->disk[c->cur], c->n[c->cur]);
 }
 
+int pmc_init_lattice_global(pmc_ctx* c, int64_t n_atoms_total) {
+    if (!c || n_atoms_total < 0) return fail(PMC_ERR_ARG, "bad argument");
+    if (n_atoms_total > c->r_cap) {
+        if (c->d_r) PMC_HIP(hipFree(c->d_r));
+        c->d_r = nullptr;
+        PMC_HIP(hipMalloc(&c->d_r, sizeof(float) * 3 * (size_t)(n_atoms_total > 0 ? n_atoms_total : 1)));
+        c->r_cap = n_atoms_total;
+    }
+    // init_r over the whole periodic box (z0 = 0, all cps_z planes): the same floats as a
+    // whole-box context's lattice
+    DevGeom gg = c->G;
+    gg.z0 = 0;
+    gg.nz_local = c->P.cps_z;
+    hipError_t e = launch_init_r(gg, n_atoms_total, icbrt_ceil(n_atoms_total), c->d_r, c->stream);
+    if (e != hipSuccess) return hip_fail(e, "init_r launch");
+    PMC_HIP(hipMemsetAsync(c->n[c->cur], 0, n_bytes(c), c->stream));
+    if (!c->tmp_cnt) {
+        PMC_HIP(hipMalloc(&c->tmp_cnt, sizeof(int32_t) * (size_t)c->cells));
+        PMC_HIP(hipMalloc(&c->tmp_idx, sizeof(int32_t) * (size_t)c->cells * (size_t)c->P.nmax));
+    }
+    PMC_HIP(hipMemsetAsync(c->flags, 0, 16, c->stream));
+    // assign keeps the owned planes' particles (clip: other slabs' particles are skipped)
+    e = launch_assign(c->G, c->d_r, n_atoms_total, c->disk[c->cur], c->n[c->cur], c->tmp_cnt, c->tmp_idx,
+                      c->flags, c->stream, 1);
+    if (e != hipSuccess) return hip_fail(e, "assign launch");
+    uint32_t fl = 0;
+    PMC_HIP(hipMemcpyAsync(&fl, c->flags, 4, hipMemcpyDeviceToHost, c->stream));
+    PMC_HIP(hipStreamSynchronize(c->stream));
+    if (fl & 4u) return fail(PMC_ERR_RANGE, "assign: particle outside the box");
+    if (fl & 2u) return fail(PMC_ERR_OVERFLOW, "assign: cell occupancy exceeds nmax");
+    return PMC_OK;
+}
+
 int pmc_phase_range(pmc_ctx* c, int colour, uint32_t sweep, int zl_begin, int zl_end) {
     if (!c || colour < 0 || colour > 7) return fail(PMC_ERR_ARG, "bad argument");
     int o[3];

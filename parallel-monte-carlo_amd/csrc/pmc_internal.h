@@ -63,7 +63,7 @@ hipError_t launch_shift(const DevGeom& g, const float* din, const int16_t* nin, 
                         int16_t* nout, int f, float d, uint32_t* flags, hipStream_t st);
 hipError_t launch_init_r(const DevGeom& g, int64_t n_atoms, int64_t n_cube, float* r, hipStream_t st);
 hipError_t launch_assign(const DevGeom& g, const float* r, int64_t n_atoms, float* disk, int16_t* n,
-                         int32_t* tmp_cnt, int32_t* tmp_idx, uint32_t* flags, hipStream_t st);
+                         int32_t* tmp_cnt, int32_t* tmp_idx, uint32_t* flags, hipStream_t st, int clip = 0);
 hipError_t launch_energy(const DevGeom& g, const float* disk, const int16_t* n,
                          unsigned long long* acc, hipStream_t st);
 hipError_t launch_selftest(const uint32_t* words, int count, float* out_f, double* out_d,

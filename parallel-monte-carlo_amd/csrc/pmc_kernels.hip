@@ -8,7 +8,7 @@
 //     periodic image (apply_PBC, subsweep.h:139-151) folded into the staged coordinates;
 //   * per trial move the lanes test old and new distances of the partners (lane = partner index
 //     mod 64), evaluate the pair energies of the compacted in-cutoff pairs, and the wave reduces
-//     dE with DPP / permlane (no barrier); accept/reject is wave-uniform and in-kernel;
+//     dE with DPP row operations (no barrier); accept/reject is wave-uniform and in-kernel;
 //   * Philox4x32-10 counter slots give every (sweep, cell, move) its own random numbers, so
 //     results are independent of launch geometry and identical to the CPU oracle.
 // No MFMA: this is not a dense contraction (pair energies are gathered, cut-off, divided).
@@ -43,30 +43,27 @@ namespace {
 __device__ __forceinline__ float as_f(int v) { return __builtin_bit_cast(float, v); }
 __device__ __forceinline__ int as_i(float v) { return __builtin_bit_cast(int, v); }
 
-// Wave-wide float sum with a FIXED xor-butterfly order (1,2,4,8,16,32).  Every lane ends with
-// the same bits; the oracle replays exactly this tree (oracle/pmc_oracle.c subsweep_cell).
-// Mirror DPP patterns are used for the xor-4 / xor-8 steps: after the previous steps all lanes of
-// a quad (resp. half-row) hold equal values, so l^7 / l^15 supply the same operand as l^4 / l^8.
-// The xor-16 / xor-32 steps use gfx950's v_permlane16_swap / v_permlane32_swap: with both
-// operands = v the swapped pair holds (own, partner) and their sum is the butterfly step in every
-// lane (float add is commutative, so both lanes of a pair get identical bits).  No LDS, no SGPR.
-__device__ __forceinline__ float wave_sum_fixed_order(float v) {
+__device__ __forceinline__ int wave_uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Wave-wide float sum in a FIXED order, the xor butterfly 1, 2, 4, 8, 16, 32 the oracle replays
+// (oracle/pmc_oracle.c subsweep_cell), delivered to an SGPR.  In-row steps: quad_perm DPP for xor 1
+// and 2, then mirror patterns for xor 4 / 8 (after the previous steps all lanes of a quad, resp.
+// half-row, hold equal values, so l^7 / l^15 supply the same operand as l^4 / l^8); every lane of
+// row r then holds the row sum r_r.  Across rows, gfx9's row_bcast:15 (rows 1 and 3 add lane 15 of
+// the row below: r1+r0, r3+r2) and row_bcast:31 (rows 2 and 3 add lane 31) leave (r3+r2)+(r1+r0)
+// in lane 63 -- the butterfly's (r0+r1)+(r2+r3) bit for bit, as float addition is commutative.
+// No LDS; only lane 63's value is meaningful (read into an SGPR).
+__device__ __forceinline__ float wave_sum_fixed_order_s(float v) {
     v = v + as_f(__builtin_amdgcn_update_dpp(0, as_i(v), 0xB1, 0xF, 0xF, true));   // quad_perm 1,0,3,2
     v = v + as_f(__builtin_amdgcn_update_dpp(0, as_i(v), 0x4E, 0xF, 0xF, true));   // quad_perm 2,3,0,1
     v = v + as_f(__builtin_amdgcn_update_dpp(0, as_i(v), 0x141, 0xF, 0xF, true));  // row_half_mirror
     v = v + as_f(__builtin_amdgcn_update_dpp(0, as_i(v), 0x140, 0xF, 0xF, true));  // row_mirror
-    {
-        const auto r = __builtin_amdgcn_permlane16_swap((unsigned)as_i(v), (unsigned)as_i(v), false, false);
-        v = as_f((int)r[0]) + as_f((int)r[1]);                                // xor 16
-    }
-    {
-        const auto r = __builtin_amdgcn_permlane32_swap((unsigned)as_i(v), (unsigned)as_i(v), false, false);
-        v = as_f((int)r[0]) + as_f((int)r[1]);                                // xor 32
-    }
-    return v;
+    // row-masked DPP adds written directly (the builtins above would not fuse a row-masked DPP
+    // move into the add); s_nop 1 = the two wait states between a VALU write and a DPP read
+    asm volatile("s_nop 1\n\tv_add_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf" : "+v"(v));
+    asm volatile("s_nop 1\n\tv_add_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf" : "+v"(v));
+    return as_f(__builtin_amdgcn_readlane(as_i(v), 63));
 }
-
-__device__ __forceinline__ int wave_uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // number of set bits of the 64-lane mask m below this lane (+ add)
 __device__ __forceinline__ int mbcnt64_add(unsigned long long m, int add) {
@@ -194,7 +191,7 @@ __device__ __forceinline__ int64_t sidx(const DevGeom& g, int x, int y, int zl) 
 //      partner 64*block + l; the pairs within the cutoff (about 1 in 5) are compacted by
 //      ballot + mbcnt into an LDS term list (new terms, then old terms with the sign bit set),
 //      and only those reach the reciprocal -- term t on lane t % 64; one fixed-order
-//      DPP/permlane reduction gives dE; accept in-kernel, wave-uniformly;
+//      DPP reduction gives dE; accept in-kernel, wave-uniformly;
 //   5. write back the own cell; one atomic per counter per wave.
 // LDS per wave (capacity lcap): x, y, z rows of `stride` = subsweep_stride(lcap) slots, then the
 // term list (2 * lcap + 64 floats; the extra 64 hold the kPad entries after the list, so a pass
@@ -503,9 +500,7 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
                 for (int t0 = 0; t0 < C; t0 += kWave) acc = acc + lj4_signed_max(buf[t0 + lane], r2min);
                 // quarter energies were accumulated; the factor 4 is exact, so 4*(sum of u)
                 // equals the sum of the 4u the oracle accumulates, bit for bit
-                const float dE = wave_sum_fixed_order(4.0f * acc);
-                // dE is wave-uniform (every lane holds the butterfly total): make that explicit
-                const float dEu = as_f(__builtin_amdgcn_readfirstlane(as_i(dE)));
+                const float dEu = wave_sum_fixed_order_s(4.0f * acc);   // SGPR
                 const bool acc_mv = beta_d * (double)dEu < (double)Tm;   // accept_move, subsweep.h:209-216
                 px_[si] = acc_mv ? qx : xi;                              // (every lane, same value)
                 if (acc_mv) {
@@ -731,14 +726,18 @@ __device__ int bin_axis(float xv, int cps, float w) {
 
 __global__ void k_assign_count(DevGeom g, const float* __restrict__ r, int64_t n_atoms,
                                int32_t* __restrict__ tmp_cnt, int32_t* __restrict__ tmp_idx,
-                               uint32_t* __restrict__ flags) {
+                               uint32_t* __restrict__ flags, int clip) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_atoms) return;
     const int cx = bin_axis(r[i], g.cps_x, g.w);
     const int cy = bin_axis(r[i + n_atoms], g.cps_y, g.w);
     const int cz = bin_axis(r[i + 2 * n_atoms], g.cps_z, g.w);
-    if (cx < 0 || cy < 0 || cz < 0 || cz < g.z0 || cz >= g.z0 + g.nz_local) {
+    if (cx < 0 || cy < 0 || cz < 0) {
         atomicOr(flags, 4u);
+        return;
+    }
+    if (cz < g.z0 || cz >= g.z0 + g.nz_local) {   // another slab's particle
+        if (!clip) atomicOr(flags, 4u);
         return;
     }
     const int64_t c = sidx(g, cx, cy, cz - g.z0);
@@ -939,13 +938,13 @@ hipError_t launch_init_r(const DevGeom& g, int64_t n_atoms, int64_t n_cube, floa
 }
 
 hipError_t launch_assign(const DevGeom& g, const float* r, int64_t n_atoms, float* disk, int16_t* n,
-                         int32_t* tmp_cnt, int32_t* tmp_idx, uint32_t* flags, hipStream_t st) {
+                         int32_t* tmp_cnt, int32_t* tmp_idx, uint32_t* flags, hipStream_t st, int clip) {
     const int64_t cells = (int64_t)g.cps_x * g.cps_y * (g.nz_local + 2 * g.halo);
     hipError_t e = hipMemsetAsync(tmp_cnt, 0, sizeof(int32_t) * (size_t)cells, st);
     if (e != hipSuccess) return e;
     if (n_atoms > 0) {
         dim3 grid((unsigned)((n_atoms + 255) / 256)), block(256);
-        hipLaunchKernelGGL(k_assign_count, grid, block, 0, st, g, r, n_atoms, tmp_cnt, tmp_idx, flags);
+        hipLaunchKernelGGL(k_assign_count, grid, block, 0, st, g, r, n_atoms, tmp_cnt, tmp_idx, flags, clip);
     }
     dim3 grid2((unsigned)((cells + 255) / 256)), block2(256);
     hipLaunchKernelGGL(k_assign_fill, grid2, block2, 0, st, g, r, n_atoms, tmp_cnt, tmp_idx, disk, n, cells);

@@ -103,6 +103,7 @@ def lib():
         _sig(L, "pmc_subsweep", i32, _vp, _vp, _vp, C.POINTER(C.c_int * 3), u32)
         _sig(L, "pmc_shift_cells", i32, _vp, _vp, _vp, _vp, _vp, i32, C.c_float)
         _sig(L, "pmc_init_lattice", i32, _vp, i64)
+        _sig(L, "pmc_init_lattice_global", i32, _vp, i64)
         _sig(L, "pmc_sweep", i32, _vp, u32)
         _sig(L, "pmc_phase", i32, _vp, i32, u32)
         _sig(L, "pmc_phase_range", i32, _vp, i32, u32, i32, i32)

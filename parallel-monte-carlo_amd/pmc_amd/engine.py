@@ -140,6 +140,10 @@ class PmcContext:
     def init_lattice(self, n_atoms: int) -> None:
         check("pmc_init_lattice", lib().pmc_init_lattice(self._h, n_atoms))
 
+    def init_lattice_global(self, n_atoms_total: int) -> None:
+        """Strong-scaling start: the whole box's lattice, this slab's planes (pmc_init_lattice_global)."""
+        check("pmc_init_lattice_global", lib().pmc_init_lattice_global(self._h, n_atoms_total))
+
     def sweep(self, s: int) -> None:
         check("pmc_sweep", lib().pmc_sweep(self._h, s))
 

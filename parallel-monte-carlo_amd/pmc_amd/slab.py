@@ -111,8 +111,10 @@ class SlabSimulation:
     # ---- construction of the product path -------------------------------------------------
     @classmethod
     def create(cls, cps: int, nz_local: int, rank: int, world: int, stream=None, atoms_per_rank: int = 0,
-               nmax: int = 16, n_moves: int = 10, seed: int = 1234, group=None, **kw):
-        """HIP engine on the current device; state in torch device tensors; RCCL transport."""
+               nmax: int = 16, n_moves: int = 10, seed: int = 1234, group=None, atoms_total: int = 0, **kw):
+        """HIP engine on the current device; state in torch device tensors; RCCL transport.
+        atoms_per_rank: a lattice inside every slab (weak scaling); atoms_total: one lattice over
+        the whole box, each rank keeping its planes (strong scaling; equals a 1-GPU run's state)."""
         import torch
         from .engine import PmcContext
         g = SlabGeometry(cps, nz_local, rank, world, nmax)
@@ -131,7 +133,10 @@ class SlabSimulation:
         if world > 1:
             import torch.distributed as dist
             dist.barrier(group=group)      # a collective first, then point-to-point (NCCL rule)
-        if atoms_per_rank:
+        if atoms_total:
+            ctx.init_lattice_global(atoms_total)
+            sim.exchange_full()
+        elif atoms_per_rank:
             ctx.init_lattice(atoms_per_rank)
             sim.exchange_full()
         return sim

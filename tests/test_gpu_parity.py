@@ -253,3 +253,27 @@ def test_gpu_slab_single_rank_equals_whole_box(pmc):
     assert sim.ctx.stats() == whole.stats()
     # energies: slab pairs across the (self-)boundary count half on each side -> same total
     assert sim.ctx.energy() == pytest.approx(whole.energy(), rel=1e-12, abs=1e-9)
+
+
+@pytest.mark.gpu
+def test_gpu_init_lattice_global_slab_planes(pmc, oracle):
+    """Strong-scaling start state (bench --strong): a slab's pmc_init_lattice_global holds exactly
+    the owned planes of the whole-box lattice, slot for slot; the slabs together hold every particle."""
+    cps, atoms, nz = 16, 10_000, 8
+    whole = pmc.PmcContext(cps)
+    whole.init_lattice(atoms)
+    dw, nw = whole.copy_out()
+    plane = cps * cps
+    total = 0
+    for z0 in (0, nz):
+        sl = pmc.PmcContext(cps, cps_z=cps, nz_local=nz, z0=z0, halo=1)
+        sl.init_lattice_global(atoms)
+        d, n = sl.copy_out()
+        own = slice(plane, plane * (nz + 1))
+        ref = slice(z0 * plane, (z0 + nz) * plane)
+        assert np.array_equal(n[own], nw[ref])
+        row = 3 * 16
+        assert oracle.valid_slots_equal(d[own.start * row:own.stop * row], n[own],
+                                        dw[ref.start * row:ref.stop * row], nw[ref], 16)
+        total += int(n[own].sum())
+    assert total == atoms
