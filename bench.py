@@ -118,7 +118,14 @@ def main() -> int:
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--graph", action="store_true", help="replay the timed sweeps as one hipGraph")
+    ap.add_argument("--no-events", action="store_true",
+                    help="no per-launch HIP events in the timed region (no roofline; overhead check)")
     ap.add_argument("--slab", action="store_true", help="use the z-slab/halo path even with one rank")
+    ap.add_argument("--slab-driver", choices=["c", "python"], default="c",
+                    help="multi-GPU driver: the C slab driver with RCCL (product) or the Python schedule "
+                         "over torch.distributed")
+    ap.add_argument("--self-rccl", action="store_true",
+                    help="one rank with --slab: halos through a one-rank RCCL communicator (rehearsal)")
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling (BASELINE config 4): one cps^3 box of --atoms particles split into "
                          "world z-slabs of cps/world planes (default: weak, cps^3 and --atoms per GPU)")
@@ -153,14 +160,16 @@ def main() -> int:
         raise SystemExit(f"slab thickness {nz_local} must be even and >= 2")
     events = []      # (kind, start, end) HIP events on the kernels' stream
 
-    def timer(kind, fn, record):
-        if not record:
+    def timer(kind, fn, record, on=None):
+        """HIP events around one launch, on the stream it is launched on (default: the kernels')."""
+        if not record or args.no_events:
             return fn()
+        st = on if on is not None else stream
         a = torch.cuda.Event(enable_timing=True)
         b = torch.cuda.Event(enable_timing=True)
-        a.record(stream)
+        a.record(st)
         fn()
-        b.record(stream)
+        b.record(st)
         events.append((kind, a, b))
 
     if not slab:
@@ -179,7 +188,21 @@ def main() -> int:
         def finish():
             pass
         cps_z = cps
+    elif args.slab_driver == "c":
+        # the product multi-GPU path: sweep schedule + RCCL halo exchange in C (pmc_slab_*)
+        from pmc_amd.slab import SlabDriver
+        drv = SlabDriver(cps=cps, nz_local=nz_local, rank=rank, world=world, stream=stream,
+                         atoms_per_rank=0 if args.strong else atoms_local,
+                         atoms_total=args.atoms if args.strong else 0, use_rccl=world > 1 or args.self_rccl)
+        sim = drv.ctx
+
+        def one_sweep(s, record):
+            drv.sweep(s)
+
+        finish = drv.finish
+        cps_z = nz_local * world
     else:
+        # the same schedule in Python over torch.distributed (comparison)
         from pmc_amd.slab import SlabSimulation
         sim_s = SlabSimulation.create(cps=cps, nz_local=nz_local, rank=rank, world=world, stream=stream,
                                       atoms_per_rank=0 if args.strong else atoms_local,
@@ -187,10 +210,11 @@ def main() -> int:
         sim = sim_s.ctx
 
         def one_sweep(s, record):
-            sim_s.sweep(s, timer=lambda kind, fn: timer(kind, fn, record))
+            sim_s.sweep(s, timer=lambda kind, fn, on=None: timer(kind, fn, record, on))
 
         finish = sim_s.finish
         cps_z = nz_local * world
+    c_slab = slab and args.slab_driver == "c"
 
     # warmup
     for s in range(args.warmup):
@@ -219,6 +243,8 @@ def main() -> int:
     abytes = algorithmic_bytes_per_sweep(n_owned, stencil)
     e_start = sim.energy()      # cell-list energy of the state the timed region starts from
 
+    if c_slab:
+        sim.slab_timing(not args.no_events)    # per-launch HIP events inside the C driver
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -239,6 +265,10 @@ def main() -> int:
     phase_total_ms = sum(a.elapsed_time(b) for kind, a, b in events if kind == "phase")
     shift_total_ms = sum(a.elapsed_time(b) for kind, a, b in events if kind == "shift")
     n_phases = 8 * args.steps if events else 0
+    if c_slab:
+        tm = sim.slab_timing(False)
+        phase_total_ms, shift_total_ms = tm["subsweep_ms"], tm["shift_ms"]
+        n_phases = 8 * args.steps if tm["n_subsweep"] else 0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -298,7 +328,10 @@ def main() -> int:
                                    f", full checkerboard sweep (8 colour phases + shiftCells), box {cps}x{cps}x{cps_z}",
                        "cells_per_gpu": cps * cps * nzl, "particles_per_gpu": atoms_local, "n_moves": 10,
                        "nmax": 16, "beta": 0.3, "sigma": 0.5, "w": 2.5,
-                       "parallelism": f"z-slab x{world}, {nzl} planes per rank (RCCL halo planes)" if slab else "single GPU"},
+                       "parallelism": (f"z-slab x{world}, {nzl} planes per rank, halo planes over "
+                                       + ("RCCL (C driver)" if c_slab and (world > 1 or args.self_rccl) else
+                                          "local copies (C driver)" if c_slab else "torch.distributed"))
+                                      if slab else "single GPU"},
             "sweeps_per_s": sweeps_per_s,
             "acceptance": st["accepted"] / st["trials"] if st["trials"] else None,
             "energy": {"start": e_start, "end": e_end, "start_plus_sum_dE": e_start + de_timed,

@@ -136,6 +136,39 @@ int pmc_shift(pmc_ctx* ctx, uint32_t sweep);
 int pmc_subsweep_range(pmc_ctx* ctx, float* d_disk, const int16_t* d_n, const int offset[3],
                        uint32_t sweep, int zl_begin, int zl_end);
 int pmc_phase_range(pmc_ctx* ctx, int colour, uint32_t sweep, int zl_begin, int zl_end);
+/* pmc_phase_range launched on `stream` (a hipStream_t; NULL = the default stream) instead of the
+ * context stream, with its own overflow queue, so it may run concurrently with a context-stream
+ * launch of the same colour on other planes (the slab driver's boundary planes beside the
+ * interior).  The caller orders the two streams between phases. */
+int pmc_phase_range_on(pmc_ctx* ctx, int colour, uint32_t sweep, int zl_begin, int zl_end, void* stream);
+/* ---- multi-GPU slab driver (one process per GPU; RCCL over xGMI) -------------------------
+ * Replaces the reference's single-GPU main loop (start.cu:237-260) for a box split into z-slabs:
+ * rank r owns planes [r*nz_local, (r+1)*nz_local) of a cps_x x cps_y x (world*nz_local) periodic
+ * box (context created with halo = 1, z0 = r*nz_local) plus a halo plane below and above.  The
+ * whole sweep schedule runs in C: interior planes on the context stream, the boundary plane of
+ * each colour phase on an auxiliary stream beside it, and only that colour's quarter of the
+ * boundary plane sent to the neighbour (RCCL send/recv) while the next interior runs.  Every rank
+ * derives the sweep plan itself and RNG counters use global cell ids, so any world size
+ * reproduces the single-GPU run bit for bit.  librccl is dlopen'ed ("librccl.so.1", or the path
+ * in PMC_RCCL_LIB). */
+/* rank 0: a fresh RCCL unique id (128 bytes) to broadcast to the other ranks */
+int pmc_comm_unique_id(unsigned char id[128]);
+/* Attach the slab driver: create the RCCL communicator (collective over the world ranks; id from
+ * rank 0), the auxiliary stream and the halo buffers.  id = NULL with world = 1: no RCCL, the
+ * periodic halos are local copies. */
+int pmc_slab_init(pmc_ctx* ctx, int rank, int world, const unsigned char* id);
+/* Refill both halo planes and their counts from the neighbours (after init_lattice, copy_in or
+ * load_snapshot).  Collective. */
+int pmc_slab_exchange(pmc_ctx* ctx);
+/* One full sweep (8 colour phases with halo exchange + shiftCells + halo refresh).  Asynchronous;
+ * collective (every rank calls it with the same sweep index). */
+int pmc_slab_sweep(pmc_ctx* ctx, uint32_t sweep);
+/* Order the context stream after the outstanding exchanges (before reading state or halos). */
+int pmc_slab_finish(pmc_ctx* ctx);
+/* Sum of the HIP-event durations of the subsweep and shift launches since the last call
+ * (synchronizes), then switch per-launch events on (enable = 1) or off. */
+int pmc_slab_timing(pmc_ctx* ctx, int enable, double* subsweep_ms, int* n_subsweep, double* shift_ms,
+                    int* n_shift);
 /* The per-sweep plan every rank replicates (no broadcast): colour order (FY_Shuffle + itoa,
  * start.cu:34-44,153-157, reseeded from time() in the reference) and the shift axis/distance
  * (kernel.cu:683-684), all from the host Philox stream keyed by `seed`. */

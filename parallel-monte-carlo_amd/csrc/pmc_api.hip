@@ -16,7 +16,10 @@
 
 using namespace pmc;
 
+struct pmc_slab;   // multi-GPU slab driver state (pmc_slab_init)
+
 struct pmc_ctx {
+    pmc_slab* slab = nullptr;
     pmc_params P;
     DevGeom G;
     int64_t cells = 0;              // storage cells (incl. halo planes)
@@ -28,6 +31,8 @@ struct pmc_ctx {
     unsigned long long* eacc = nullptr;    // kStatSlots (energy)
     uint32_t* flags = nullptr;
     int* ovf = nullptr;                    // subsweep overflow queue (1 + cells per colour)
+    int* ovf_aux = nullptr;                // second queue: launches on a caller stream (pmc_phase_range_on)
+    size_t ovf_bytes = 0;
     int32_t* tmp_cnt = nullptr;
     int32_t* tmp_idx = nullptr;
     float* d_r = nullptr;
@@ -135,6 +140,8 @@ void drop_graph(pmc_ctx* c) {
     c->graph_count = 0;
 }
 
+void drop_slab(pmc_ctx* c);
+
 int enqueue_sweep(pmc_ctx* c, uint32_t sweep) {
     const pmc_sweep_plan_t plan = pmc_plan_for_sweep(c->P.seed, sweep, c->P.w);
     for (int k = 0; k < 8; ++k) {
@@ -196,6 +203,7 @@ int pmc_create(const pmc_params* params, pmc_ctx** out) {
         const size_t ob = sizeof(int) * (kOvfHead + per_colour);
         if ((e = hipMalloc(&c->ovf, ob)) != hipSuccess) return cleanup(hip_fail(e, "hipMalloc ovf"));
         if ((e = hipMemset(c->ovf, 0, ob)) != hipSuccess) return cleanup(hip_fail(e, "hipMemset"));
+        c->ovf_bytes = ob;
     }
     if ((e = hipMemset(c->flags, 0, 16)) != hipSuccess) return cleanup(hip_fail(e, "hipMemset"));
     if ((e = hipEventCreate(&c->ev0)) != hipSuccess) return cleanup(hip_fail(e, "hipEventCreate"));
@@ -207,12 +215,14 @@ int pmc_create(const pmc_params* params, pmc_ctx** out) {
 void pmc_destroy(pmc_ctx* c) {
     if (!c) return;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    drop_slab(c);
     drop_graph(c);
     free_state(c);
     if (c->stats) (void)hipFree(c->stats);
     if (c->eacc) (void)hipFree(c->eacc);
     if (c->flags) (void)hipFree(c->flags);
     if (c->ovf) (void)hipFree(c->ovf);
+    if (c->ovf_aux) (void)hipFree(c->ovf_aux);
     if (c->tmp_cnt) (void)hipFree(c->tmp_cnt);
     if (c->tmp_idx) (void)hipFree(c->tmp_idx);
     if (c->d_r) (void)hipFree(c->d_r);
@@ -368,6 +378,23 @@ int pmc_phase_range(pmc_ctx* c, int colour, uint32_t sweep, int zl_begin, int zl
     int o[3];
     pmc_colour_offset(colour, o);
     return pmc_subsweep_range(c, c->disk[c->cur], c->n[c->cur], o, sweep, zl_begin, zl_end);
+}
+
+int pmc_phase_range_on(pmc_ctx* c, int colour, uint32_t sweep, int zl_begin, int zl_end, void* stream) {
+    if (!c || colour < 0 || colour > 7) return fail(PMC_ERR_ARG, "bad argument");
+    if (zl_begin < 0 || zl_end > c->P.nz_local || zl_begin > zl_end)
+        return fail(PMC_ERR_ARG, "plane range outside the owned planes");
+    hipStream_t st = (hipStream_t)stream;
+    if (st == c->stream) return pmc_phase_range(c, colour, sweep, zl_begin, zl_end);
+    if (!c->ovf_aux) {   // the aux launches' own overflow queue (concurrent with the context stream's)
+        PMC_HIP(hipMalloc(&c->ovf_aux, c->ovf_bytes));
+        PMC_HIP(hipMemset(c->ovf_aux, 0, c->ovf_bytes));
+    }
+    int o[3];
+    pmc_colour_offset(colour, o);
+    hipError_t e = launch_subsweep(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep, c->stats,
+                                   c->ovf_aux, zl_begin, zl_end, st);
+    return e == hipSuccess ? PMC_OK : hip_fail(e, "subsweep launch");
 }
 
 int pmc_phase(pmc_ctx* c, int colour, uint32_t sweep) {
@@ -647,3 +674,349 @@ int pmc_load_snapshot(pmc_ctx* c, const char* path, uint32_t* next_sweep) {
     if (next_sweep) *next_sweep = sw;
     return PMC_OK;
 }
+
+// =========================================================================================
+// Multi-GPU slab driver: one process per GPU, each owning a z-slab of the box
+// plus one halo plane below and above; halos travel over RCCL (xGMI) point-to-point.
+// The whole sweep schedule runs here, in C: per colour phase a handful of HIP/RCCL calls and no
+// Python, so the host stays ahead of the GPU even for thin (strong-scaling) slabs.
+// =========================================================================================
+#include <dlfcn.h>
+#include <rccl/rccl.h>   // types and signatures only: librccl is dlopen'ed by soname, so a
+                         // process that already holds one (torch's) shares that instance
+
+namespace {
+
+struct Rccl {
+    bool tried = false, ok = false;
+    std::string err;
+    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+    decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+    decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclSend) send = nullptr;
+    decltype(&ncclRecv) recv = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+};
+
+Rccl& rccl() {
+    static Rccl r;
+    if (r.tried) return r;
+    r.tried = true;
+    const char* path = std::getenv("PMC_RCCL_LIB");
+    void* h = dlopen(path && *path ? path : "librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+        r.err = std::string("dlopen librccl: ") + dlerror();
+        return r;
+    }
+    auto sym = [&](const char* name) { return dlsym(h, name); };
+    r.get_unique_id = (decltype(r.get_unique_id))sym("ncclGetUniqueId");
+    r.comm_init_rank = (decltype(r.comm_init_rank))sym("ncclCommInitRank");
+    r.comm_destroy = (decltype(r.comm_destroy))sym("ncclCommDestroy");
+    r.send = (decltype(r.send))sym("ncclSend");
+    r.recv = (decltype(r.recv))sym("ncclRecv");
+    r.group_start = (decltype(r.group_start))sym("ncclGroupStart");
+    r.group_end = (decltype(r.group_end))sym("ncclGroupEnd");
+    r.error_string = (decltype(r.error_string))sym("ncclGetErrorString");
+    r.ok = r.get_unique_id && r.comm_init_rank && r.comm_destroy && r.send && r.recv && r.group_start &&
+           r.group_end && r.error_string;
+    if (!r.ok) r.err = "librccl lacks a required symbol";
+    return r;
+}
+
+int nccl_fail(ncclResult_t e, const char* what) {
+    return fail(PMC_ERR_HIP, std::string(what) + ": " + rccl().error_string(e));
+}
+
+#define PMC_NCCL(call)                                    \
+    do {                                                  \
+        ncclResult_t r_ = (call);                         \
+        if (r_ != ncclSuccess) return nccl_fail(r_, #call); \
+    } while (0)
+
+}  // namespace
+
+struct pmc_slab {
+    int rank = 0, world = 1, below = 0, above = 0;
+    ncclComm_t comm = nullptr;            // null: one rank, halos by local copies
+    hipStream_t aux = nullptr;            // boundary planes + exchanges ("T")
+    hipEvent_t ev_i = nullptr, ev_b = nullptr, ev_t = nullptr;
+    float* sbuf = nullptr;                // packed colour cells of the sent plane
+    float* rbuf = nullptr;                // ... of the received plane
+    size_t pack_floats = 0;
+    int pend_colour = -1, pend_dst = 0;   // unpack owed on aux (colour, halo plane)
+    bool timing = false;                  // HIP events around every subsweep / shift launch
+    std::vector<hipEvent_t> tev;          // pool: (start, end) pairs
+    std::vector<int> tkind;               // 0 subsweep, 1 shift, per pair in use
+};
+
+namespace {
+
+void drop_slab(pmc_ctx* c) {
+    pmc_slab* s = c->slab;
+    if (!s) return;
+    if (s->aux) (void)hipStreamSynchronize(s->aux);
+    if (s->comm && rccl().ok) (void)rccl().comm_destroy(s->comm);
+    if (s->aux) (void)hipStreamDestroy(s->aux);
+    for (hipEvent_t e : {s->ev_i, s->ev_b, s->ev_t})
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : s->tev) (void)hipEventDestroy(e);
+    if (s->sbuf) (void)hipFree(s->sbuf);
+    if (s->rbuf) (void)hipFree(s->rbuf);
+    delete s;
+    c->slab = nullptr;
+}
+
+size_t plane_floats(const pmc_ctx* c) { return (size_t)c->P.cps_x * c->P.cps_y * 3 * c->P.nmax; }
+size_t plane_cells(const pmc_ctx* c) { return (size_t)c->P.cps_x * c->P.cps_y; }
+// storage plane of local plane z (-1 = bottom halo, nz_local = top halo)
+float* disk_plane(pmc_ctx* c, int z) { return c->disk[c->cur] + (size_t)(z + 1) * plane_floats(c); }
+int16_t* n_plane(pmc_ctx* c, int z) { return c->n[c->cur] + (size_t)(z + 1) * plane_cells(c); }
+
+// one timed launch: events around `launch` on stream st when timing is on
+template <class F>
+hipError_t timed(pmc_slab* s, int kind, hipStream_t st, F&& launch) {
+    if (!s->timing) return launch();
+    const size_t k = s->tkind.size();
+    while (s->tev.size() < 2 * (k + 1)) {
+        hipEvent_t e;
+        hipError_t r = hipEventCreate(&e);
+        if (r != hipSuccess) return r;
+        s->tev.push_back(e);
+    }
+    s->tkind.push_back(kind);
+    hipError_t r = hipEventRecord(s->tev[2 * k], st);
+    if (r != hipSuccess) return r;
+    r = launch();
+    if (r != hipSuccess) return r;
+    return hipEventRecord(s->tev[2 * k + 1], st);
+}
+
+// finish the previous phase exchange on aux: unpack the received colour cells into the halo
+int slab_complete(pmc_ctx* c) {
+    pmc_slab* s = c->slab;
+    if (s->pend_colour < 0) return PMC_OK;
+    hipError_t e = launch_colour_rows(c->G, s->rbuf, disk_plane(c, s->pend_dst), s->pend_colour, 1, s->aux);
+    s->pend_colour = -1;
+    return e == hipSuccess ? PMC_OK : hip_fail(e, "unpack launch");
+}
+
+// after colour phase `colour`: its boundary plane (z-parity oz = colour % 2, start.cu:153-157)
+// goes to the neighbour that holds it as a halo; the matching halo comes from the other side.
+// Only that colour's quarter of the plane changed, so only it travels: the boundary launch wrote
+// those rows packed into sbuf (mirror rows); the received ones are unpacked by slab_complete.
+// A single rank needs nothing here: its boundary launch mirrored the rows into its own halo.
+int slab_exchange_phase(pmc_ctx* c, int colour) {
+    pmc_slab* s = c->slab;
+    if (!s->comm) return PMC_OK;
+    const bool down = colour % 2 == 0;                 // oz = 0: plane 0 -> below, top halo <- above
+    const int to = down ? s->below : s->above, from = down ? s->above : s->below;
+    Rccl& R = rccl();
+    PMC_NCCL(R.group_start());
+    PMC_NCCL(R.send(s->sbuf, s->pack_floats, ncclFloat32, to, s->comm, s->aux));
+    PMC_NCCL(R.recv(s->rbuf, s->pack_floats, ncclFloat32, from, s->comm, s->aux));
+    PMC_NCCL(R.group_end());
+    s->pend_colour = colour;
+    s->pend_dst = down ? c->P.nz_local : -1;
+    return PMC_OK;
+}
+
+// both boundary planes with their counts (after shiftCells / initialisation), on aux
+int slab_exchange_full(pmc_ctx* c) {
+    pmc_slab* s = c->slab;
+    const int nz = c->P.nz_local;
+    const size_t pf = plane_floats(c), pc = plane_cells(c);
+    if (!s->comm) {
+        PMC_HIP(hipMemcpyAsync(disk_plane(c, nz), disk_plane(c, 0), pf * 4, hipMemcpyDeviceToDevice, s->aux));
+        PMC_HIP(hipMemcpyAsync(n_plane(c, nz), n_plane(c, 0), pc * 2, hipMemcpyDeviceToDevice, s->aux));
+        PMC_HIP(hipMemcpyAsync(disk_plane(c, -1), disk_plane(c, nz - 1), pf * 4, hipMemcpyDeviceToDevice, s->aux));
+        PMC_HIP(hipMemcpyAsync(n_plane(c, -1), n_plane(c, nz - 1), pc * 2, hipMemcpyDeviceToDevice, s->aux));
+        return PMC_OK;
+    }
+    // per peer, sends and receives match in issue order: (plane, counts) down, then up
+    Rccl& R = rccl();
+    PMC_NCCL(R.group_start());
+    PMC_NCCL(R.send(disk_plane(c, 0), pf, ncclFloat32, s->below, s->comm, s->aux));
+    PMC_NCCL(R.send(n_plane(c, 0), pc * 2, ncclUint8, s->below, s->comm, s->aux));
+    PMC_NCCL(R.send(disk_plane(c, nz - 1), pf, ncclFloat32, s->above, s->comm, s->aux));
+    PMC_NCCL(R.send(n_plane(c, nz - 1), pc * 2, ncclUint8, s->above, s->comm, s->aux));
+    PMC_NCCL(R.recv(disk_plane(c, nz), pf, ncclFloat32, s->above, s->comm, s->aux));
+    PMC_NCCL(R.recv(n_plane(c, nz), pc * 2, ncclUint8, s->above, s->comm, s->aux));
+    PMC_NCCL(R.recv(disk_plane(c, -1), pf, ncclFloat32, s->below, s->comm, s->aux));
+    PMC_NCCL(R.recv(n_plane(c, -1), pc * 2, ncclUint8, s->below, s->comm, s->aux));
+    PMC_NCCL(R.group_end());
+    return PMC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pmc_comm_unique_id(unsigned char id[128]) {
+    if (!id) return fail(PMC_ERR_ARG, "null argument");
+    Rccl& R = rccl();
+    if (!R.ok) return fail(PMC_ERR_HIP, R.err);
+    ncclUniqueId u;
+    PMC_NCCL(R.get_unique_id(&u));
+    static_assert(sizeof(u) == 128, "ncclUniqueId size");
+    std::memcpy(id, &u, 128);
+    return PMC_OK;
+}
+
+int pmc_slab_init(pmc_ctx* c, int rank, int world, const unsigned char* id) {
+    if (!c || world < 1 || rank < 0 || rank >= world) return fail(PMC_ERR_ARG, "bad argument");
+    if (c->P.halo != 1) return fail(PMC_ERR_ARG, "pmc_slab_init needs a slab context (halo = 1)");
+    if (c->P.nz_local < 2 || c->P.z0 != rank * c->P.nz_local || c->P.cps_z != world * c->P.nz_local)
+        return fail(PMC_ERR_ARG, "slab geometry must be z0 = rank*nz_local, cps_z = world*nz_local");
+    if (!id && world != 1) return fail(PMC_ERR_ARG, "more than one rank needs an RCCL unique id");
+    PMC_HIP(hipStreamSynchronize(c->stream));
+    drop_slab(c);
+    pmc_slab* s = new pmc_slab();
+    c->slab = s;
+    s->rank = rank;
+    s->world = world;
+    s->below = (rank + world - 1) % world;
+    s->above = (rank + 1) % world;
+    hipError_t e;
+    if ((e = hipStreamCreateWithFlags(&s->aux, hipStreamNonBlocking)) != hipSuccess) {
+        drop_slab(c);
+        return hip_fail(e, "hipStreamCreate");
+    }
+    for (hipEvent_t* ev : {&s->ev_i, &s->ev_b, &s->ev_t})
+        if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) {
+            drop_slab(c);
+            return hip_fail(e, "hipEventCreate");
+        }
+    s->pack_floats = (size_t)(c->P.cps_x / 2) * (c->P.cps_y / 2) * 3 * c->P.nmax;
+    if (id) {
+        Rccl& R = rccl();
+        if (!R.ok) {
+            drop_slab(c);
+            return fail(PMC_ERR_HIP, R.err);
+        }
+        if ((e = hipMalloc(&s->sbuf, s->pack_floats * 4)) != hipSuccess ||
+            (e = hipMalloc(&s->rbuf, s->pack_floats * 4)) != hipSuccess) {
+            drop_slab(c);
+            return hip_fail(e, "hipMalloc halo buffers");
+        }
+        ncclUniqueId u;
+        std::memcpy(&u, id, 128);
+        ncclResult_t r = R.comm_init_rank(&s->comm, world, u, rank);
+        if (r != ncclSuccess) {
+            s->comm = nullptr;
+            int rc = nccl_fail(r, "ncclCommInitRank");
+            drop_slab(c);
+            return rc;
+        }
+    }
+    return PMC_OK;
+}
+
+int pmc_slab_exchange(pmc_ctx* c) {
+    if (!c || !c->slab) return fail(PMC_ERR_ARG, "no slab driver (pmc_slab_init)");
+    pmc_slab* s = c->slab;
+    PMC_HIP(hipEventRecord(s->ev_i, c->stream));
+    PMC_HIP(hipStreamWaitEvent(s->aux, s->ev_i, 0));
+    int rc = slab_complete(c);
+    if (rc) return rc;
+    if ((rc = slab_exchange_full(c))) return rc;
+    PMC_HIP(hipEventRecord(s->ev_t, s->aux));
+    PMC_HIP(hipStreamWaitEvent(c->stream, s->ev_t, 0));
+    return PMC_OK;
+}
+
+int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
+    if (!c || !c->slab) return fail(PMC_ERR_ARG, "no slab driver (pmc_slab_init)");
+    pmc_slab* s = c->slab;
+    hipStream_t S = c->stream, T = s->aux;
+    const int nz = c->P.nz_local;
+    const pmc_sweep_plan_t plan = pmc_plan_for_sweep(c->P.seed, sweep, c->P.w);
+    hipError_t e;
+    int rc;
+    // Per colour k:  S: wait B(k-1) -> interior I(k) = planes [1, nz-1) (reads no halo)
+    //                T: wait I(k-1) -> unpack halo of exchange k-1 -> boundary B(k) = the one
+    //                   boundary plane of parity oz -> pack + RCCL send/recv of its colour cells.
+    // I(k) and B(k) run together; exchange k overlaps I(k+1).  I(k) never writes a plane an
+    // exchange reads, nor reads a halo one writes.  Cells of a colour are independent, so any
+    // split of a phase gives the whole-box result bit for bit.
+    PMC_HIP(hipEventRecord(s->ev_i, S));                       // "I(-1)": all earlier S work
+    for (int k = 0; k < 8; ++k) {
+        const int colour = plan.order[k];
+        int o[3];
+        pmc_colour_offset(colour, o);
+        PMC_HIP(hipStreamWaitEvent(T, s->ev_i, 0));            // I(k-1)
+        if (k > 0) PMC_HIP(hipStreamWaitEvent(S, s->ev_b, 0)); // B(k-1)
+        if (nz > 2) {
+            e = timed(s, 0, S, [&] {
+                return launch_subsweep(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep, c->stats,
+                                       c->ovf, 1, nz - 1, S);
+            });
+            if (e != hipSuccess) return hip_fail(e, "subsweep launch");
+        }
+        PMC_HIP(hipEventRecord(s->ev_i, S));
+        if ((rc = slab_complete(c))) return rc;
+        // the boundary plane of this parity, full capacity (no fallback launch); its written-back
+        // rows go straight to the send buffer (RCCL) or to the periodic halo (single rank)
+        const bool down = o[2] == 0;
+        const int zb = down ? 0 : nz - 1;
+        float* mirror = s->comm ? s->sbuf : disk_plane(c, down ? nz : -1);
+        e = timed(s, 0, T, [&] {
+            return launch_subsweep_boundary(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep,
+                                            c->stats, zb, zb + 1, mirror, s->comm ? 0 : 1, T);
+        });
+        if (e != hipSuccess) return hip_fail(e, "subsweep launch");
+        PMC_HIP(hipEventRecord(s->ev_b, T));
+        if ((rc = slab_exchange_phase(c, colour))) return rc;
+    }
+    if ((rc = slab_complete(c))) return rc;
+    PMC_HIP(hipEventRecord(s->ev_t, T));
+    PMC_HIP(hipStreamWaitEvent(S, s->ev_t, 0));
+    e = timed(s, 1, S, [&] {
+        return launch_shift(c->G, c->disk[c->cur], c->n[c->cur], c->disk[c->cur ^ 1], c->n[c->cur ^ 1], plan.f,
+                            plan.d, c->flags, S);
+    });
+    if (e != hipSuccess) return hip_fail(e, "shift launch");
+    c->cur ^= 1;
+    // shiftCells moved particles across the boundary planes: refresh both halos with counts; the
+    // next sweep's first interior overlaps it, its first boundary launch follows it on T
+    PMC_HIP(hipEventRecord(s->ev_i, S));
+    PMC_HIP(hipStreamWaitEvent(T, s->ev_i, 0));
+    if ((rc = slab_exchange_full(c))) return rc;
+    PMC_HIP(hipEventRecord(s->ev_t, T));
+    return PMC_OK;
+}
+
+int pmc_slab_finish(pmc_ctx* c) {
+    if (!c || !c->slab) return fail(PMC_ERR_ARG, "no slab driver (pmc_slab_init)");
+    PMC_HIP(hipEventRecord(c->slab->ev_t, c->slab->aux));
+    PMC_HIP(hipStreamWaitEvent(c->stream, c->slab->ev_t, 0));
+    return PMC_OK;
+}
+
+int pmc_slab_timing(pmc_ctx* c, int enable, double* subsweep_ms, int* n_subsweep, double* shift_ms,
+                    int* n_shift) {
+    if (!c || !c->slab) return fail(PMC_ERR_ARG, "no slab driver (pmc_slab_init)");
+    pmc_slab* s = c->slab;
+    double a = 0.0, b = 0.0;
+    int na = 0, nb = 0;
+    if (!s->tkind.empty()) {
+        PMC_HIP(hipStreamSynchronize(s->aux));
+        PMC_HIP(hipStreamSynchronize(c->stream));
+        for (size_t k = 0; k < s->tkind.size(); ++k) {
+            float ms = 0.0f;
+            PMC_HIP(hipEventElapsedTime(&ms, s->tev[2 * k], s->tev[2 * k + 1]));
+            if (s->tkind[k] == 0) { a += ms; ++na; }
+            else { b += ms; ++nb; }
+        }
+    }
+    if (subsweep_ms) *subsweep_ms = a;
+    if (n_subsweep) *n_subsweep = na;
+    if (shift_ms) *shift_ms = b;
+    if (n_shift) *n_shift = nb;
+    s->tkind.clear();
+    s->timing = enable != 0;
+    return PMC_OK;
+}
+
+}  // extern "C"

@@ -58,6 +58,12 @@ struct DevGeom {
 hipError_t launch_subsweep(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
                            uint32_t sweep, unsigned long long* stats, int* ovf, int zl_begin, int zl_end,
                            hipStream_t st);
+// the slab driver's boundary planes: full LDS capacity (no overflow queue), every written-back row
+// also stored to `mirror` (mirror_mode 0: packed colour rows ta + tb*cps_x/2, 1: plane rows;
+// mirror may be null)
+hipError_t launch_subsweep_boundary(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
+                                    uint32_t sweep, unsigned long long* stats, int zl_begin, int zl_end,
+                                    float* mirror, int mirror_mode, hipStream_t st);
 int subsweep_capacity(const DevGeom& g);
 hipError_t launch_shift(const DevGeom& g, const float* din, const int16_t* nin, float* dout,
                         int16_t* nout, int f, float d, uint32_t* flags, hipStream_t st);
@@ -66,6 +72,9 @@ hipError_t launch_assign(const DevGeom& g, const float* r, int64_t n_atoms, floa
                          int32_t* tmp_cnt, int32_t* tmp_idx, uint32_t* flags, hipStream_t st, int clip = 0);
 hipError_t launch_energy(const DevGeom& g, const float* disk, const int16_t* n,
                          unsigned long long* acc, hipStream_t st);
+// the cells of one colour of one plane: mode 0 plane -> packed buffer, 1 packed -> plane,
+// 2 plane -> plane; (cps_x/2)*(cps_y/2)*3*nmax floats
+hipError_t launch_colour_rows(const DevGeom& g, const float* src, float* dst, int colour, int mode, hipStream_t st);
 hipError_t launch_selftest(const uint32_t* words, int count, float* out_f, double* out_d,
                            float rc2, hipStream_t st);
 

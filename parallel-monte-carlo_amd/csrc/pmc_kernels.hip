@@ -200,12 +200,16 @@ __device__ __forceinline__ int64_t sidx(const DevGeom& g, int x, int y, int zl) 
 // ------------------------------------------------------------------------------------------
 // Returns false (and leaves the cell untouched) when the cell's staged partners do not fit the
 // LDS capacity `cap`; the caller queues it for the full-capacity fallback launch.
-template <int NSLOT, int NMC, int LCAP, bool OFF32>
+// MIRROR (slab boundary planes): the written-back rows also go to `mirror` -- mirror_mode 0: the
+// packed colour buffer of the halo exchange (row ta + tb*cps_x/2), 1: a plane (row x + cps_x*y;
+// the periodic single-rank halo).  Empty cells write nothing (their count stays 0).
+template <int NSLOT, int NMC, int LCAP, bool OFF32, bool MIRROR = false>
 __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restrict__ disk,
                                               const int16_t* __restrict__ ncnt, int ox, int oy, int oz,
                                               uint32_t sweep, unsigned long long* __restrict__ stats,
                                               float* __restrict__ px_, int lcap_rt, int cap, int t,
-                                              int cz0) {
+                                              int cz0, float* __restrict__ mirror = nullptr,
+                                              int mirror_mode = 0) {
     constexpr int HS = stage_split(NSLOT);        // staging lanes per stencil cell (main passes)
     constexpr int CPP = kWave / HS;               // stencil cells staged per pass
     constexpr int NP = (26 + CPP - 1) / CPP;      // main staging passes over the 26 neighbours
@@ -523,6 +527,14 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
         A::st(disk, off, px_[S_nb + lane]);
         A::st(disk, off + (uint32_t)nm * A::kUnit, py_[S_nb + lane]);
         A::st(disk, off + 2u * (uint32_t)nm * A::kUnit, pz_[S_nb + lane]);
+        if constexpr (MIRROR) {
+            const uint32_t r = mirror_mode == 0 ? (uint32_t)ta + (uint32_t)tb * (uint32_t)(g.cps_x >> 1)
+                                                : (uint32_t)x + (uint32_t)g.cps_x * (uint32_t)y;
+            float* m = mirror + (size_t)r * (3 * nm) + lane;
+            m[0] = px_[S_nb + lane];
+            m[nm] = py_[S_nb + lane];
+            m[2 * nm] = pz_[S_nb + lane];
+        }
     }
     // fixed-point conversion only when something was accepted (pmc_to_fixed(0) == 0)
     const int64_t de_fix = n_acc ? pmc_to_fixed(de_cell) : 0;
@@ -564,6 +576,31 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep(DevGeom g, float
                                                 t, cz0)) {
         if ((threadIdx.x & (kWave - 1)) == 0) ovf[kOvfHead + atomicAdd(&ovf[kOvfCount], 1)] = t;
     }
+}
+
+// Boundary-plane launch of the slab driver: full capacity (27*nmax partners per wave: no overflow
+// queue, no fallback launch -- a plane is a small launch, occupancy is not what bounds it), one wave
+// per cell of the plane range, written-back rows mirrored into the halo exchange buffer.
+template <int NSLOT, int NMC, bool OFF32>
+__global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_direct(DevGeom g, float* __restrict__ disk,
+                                                                         const int16_t* __restrict__ ncnt,
+                                                                         int ox, int oy, int oz, uint32_t sweep,
+                                                                         unsigned long long* __restrict__ stats,
+                                                                         int cz0, int ncz, float* __restrict__ mirror,
+                                                                         int mirror_mode) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int full = 27 * (NMC > 0 ? NMC : g.nmax);
+    float* px_ = smem + wv * lds_floats_per_wave(full);
+    const int total = (g.cps_x >> 1) * (g.cps_y >> 1) * ncz;
+    const int t = (int)blockIdx.x * kSubWaves + wv;
+    if (t >= total) return;
+    if (mirror)
+        (void)subsweep_wave<NSLOT, NMC, 27 * NMC, OFF32, true>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, full,
+                                                               full, t, cz0, mirror, mirror_mode);
+    else
+        (void)subsweep_wave<NSLOT, NMC, 27 * NMC, OFF32>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, full, full,
+                                                         t, cz0);
 }
 
 // Fallback launch: full capacity (27*nmax partners per wave), a fixed grid striding over the
@@ -824,6 +861,26 @@ __global__ __launch_bounds__(256) void k_energy(DevGeom g, const float* __restri
 // ------------------------------------------------------------------------------------------
 // self-test of the deterministic math on the device (compared bitwise with the host oracle)
 // ------------------------------------------------------------------------------------------
+// ------------------------------------------------------------------------------------------
+// halo exchange (slab driver): the cells of one colour (x % 2 == ox, y % 2 == oy) of one plane --
+// the only cells a colour phase changes -- as (cps_y/2)*(cps_x/2) packed rows of 3*nmax floats.
+// mode 0: plane -> packed, 1: packed -> plane, 2: plane -> plane (single-rank periodic halo).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_colour_rows(const float* __restrict__ src, float* __restrict__ dst,
+                                                     int cps_x, int cps_y, int row, int ox, int oy, int mode) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int hx = cps_x >> 1;
+    const int64_t total = (int64_t)hx * (cps_y >> 1) * row;
+    if (i >= total) return;
+    const int f = (int)(i % row);
+    const int64_t j = i / row;
+    const int64_t cell = (2 * (j / hx) + oy) * cps_x + 2 * (j % hx) + ox;
+    const int64_t pidx = cell * row + f;
+    if (mode == 0) dst[i] = src[pidx];
+    else if (mode == 1) dst[pidx] = src[i];
+    else dst[pidx] = src[pidx];
+}
+
 __global__ void k_selftest(const uint32_t* __restrict__ words, int count, float* __restrict__ out_f,
                            double* __restrict__ out_d, float rc2) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -882,6 +939,27 @@ static void launch_subsweep_t(const DevGeom& g, float* disk, const int16_t* n, i
     }
 }
 
+template <int NSLOT, int NMC, bool OFF32>
+static void launch_direct_t(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz, uint32_t sweep,
+                            unsigned long long* stats, int cz0, int ncz, float* mirror, int mode, hipStream_t st) {
+    const int64_t total = (int64_t)(g.cps_x / 2) * (g.cps_y / 2) * ncz;
+    const int64_t blocks = (total + kSubWaves - 1) / kSubWaves;
+    const size_t lds = sizeof(float) * (size_t)lds_floats_per_wave(27 * g.nmax) * kSubWaves;
+    hipLaunchKernelGGL((k_subsweep_direct<NSLOT, NMC, OFF32>), dim3((unsigned)blocks), dim3(kWave * kSubWaves), lds,
+                       st, g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, mirror, mode);
+}
+
+template <bool OFF32>
+static void launch_direct_n(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz, uint32_t sweep,
+                            unsigned long long* stats, int cz0, int ncz, float* mirror, int mode, hipStream_t st) {
+    if (g.nmax == 16) launch_direct_t<16, 16, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, mirror, mode, st);
+    else if (g.nmax == 32) launch_direct_t<32, 32, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, mirror, mode, st);
+    else if (g.nslot == 8) launch_direct_t<8, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, mirror, mode, st);
+    else if (g.nslot == 16) launch_direct_t<16, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, mirror, mode, st);
+    else if (g.nslot == 32) launch_direct_t<32, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, mirror, mode, st);
+    else launch_direct_t<64, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, mirror, mode, st);
+}
+
 template <bool OFF32>
 static void launch_subsweep_n(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
                               uint32_t sweep, unsigned long long* stats, int* ovf, int cz0, int ncz,
@@ -892,6 +970,20 @@ static void launch_subsweep_n(const DevGeom& g, float* disk, const int16_t* n, i
     else if (g.nslot == 16) launch_subsweep_t<16, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st);
     else if (g.nslot == 32) launch_subsweep_t<32, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st);
     else launch_subsweep_t<64, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st);
+}
+
+hipError_t launch_subsweep_boundary(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
+                                    uint32_t sweep, unsigned long long* stats, int zl_begin, int zl_end,
+                                    float* mirror, int mirror_mode, hipStream_t st) {
+    auto ceil_half = [](int v) { return v <= 0 ? 0 : (v + 1) / 2; };
+    const int nczc = g.nz_local / 2;
+    int cz0 = ceil_half(zl_begin - oz), cz1 = ceil_half(zl_end - oz);
+    if (cz1 > nczc) cz1 = nczc;
+    if (cz1 <= cz0) return hipSuccess;
+    const int64_t bytes = (int64_t)g.cps_x * g.cps_y * (g.nz_local + 2 * g.halo) * 3 * g.nmax * 4;
+    if (bytes < ((int64_t)1 << 32)) launch_direct_n<true>(g, disk, n, ox, oy, oz, sweep, stats, cz0, cz1 - cz0, mirror, mirror_mode, st);
+    else launch_direct_n<false>(g, disk, n, ox, oy, oz, sweep, stats, cz0, cz1 - cz0, mirror, mirror_mode, st);
+    return hipGetLastError();
 }
 
 hipError_t launch_subsweep(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
@@ -962,6 +1054,16 @@ hipError_t launch_energy(const DevGeom& g, const float* disk, const int16_t* n,
         case 32: hipLaunchKernelGGL(k_energy<32>, grid, block, 0, st, g, disk, n, acc); break;
         default: hipLaunchKernelGGL(k_energy<64>, grid, block, 0, st, g, disk, n, acc); break;
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_colour_rows(const DevGeom& g, const float* src, float* dst, int colour, int mode, hipStream_t st) {
+    int o[3];
+    pmc_colour_offset(colour, o);
+    const int row = 3 * g.nmax;
+    const int64_t total = (int64_t)(g.cps_x / 2) * (g.cps_y / 2) * row;
+    dim3 grid((unsigned)((total + 255) / 256)), block(256);
+    hipLaunchKernelGGL(k_colour_rows, grid, block, 0, st, src, dst, g.cps_x, g.cps_y, row, o[0], o[1], mode);
     return hipGetLastError();
 }
 

@@ -107,6 +107,13 @@ def lib():
         _sig(L, "pmc_sweep", i32, _vp, u32)
         _sig(L, "pmc_phase", i32, _vp, i32, u32)
         _sig(L, "pmc_phase_range", i32, _vp, i32, u32, i32, i32)
+        _sig(L, "pmc_phase_range_on", i32, _vp, i32, u32, i32, i32, _vp)
+        _sig(L, "pmc_comm_unique_id", i32, _vp)
+        _sig(L, "pmc_slab_init", i32, _vp, i32, i32, _vp)
+        _sig(L, "pmc_slab_exchange", i32, _vp)
+        _sig(L, "pmc_slab_sweep", i32, _vp, u32)
+        _sig(L, "pmc_slab_finish", i32, _vp)
+        _sig(L, "pmc_slab_timing", i32, _vp, i32, _vp, _vp, _vp, _vp)
         _sig(L, "pmc_subsweep_range", i32, _vp, _vp, _vp, C.POINTER(C.c_int * 3), u32, i32, i32)
         _sig(L, "pmc_shift", i32, _vp, u32)
         _sig(L, "pmc_start", i32, _vp, u32, i32, C.POINTER(Result))

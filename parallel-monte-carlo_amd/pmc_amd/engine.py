@@ -153,6 +153,33 @@ class PmcContext:
     def phase_range(self, colour: int, s: int, zl_begin: int, zl_end: int) -> None:
         check("pmc_phase_range", lib().pmc_phase_range(self._h, colour, s, zl_begin, zl_end))
 
+    def phase_range_on(self, colour: int, s: int, zl_begin: int, zl_end: int, stream: int) -> None:
+        """phase_range on another HIP stream (own overflow queue): concurrent with the context
+        stream's launches of the same colour on other planes; the caller orders the streams."""
+        check("pmc_phase_range_on", lib().pmc_phase_range_on(self._h, colour, s, zl_begin, zl_end,
+                                                             C.c_void_p(stream)))
+
+    # ---- multi-GPU slab driver (pmc_slab_*: schedule + RCCL in C) ---------------------------
+    def slab_init(self, rank: int, world: int, unique_id: Optional[bytes]) -> None:
+        uid = None if unique_id is None else (C.c_ubyte * 128).from_buffer_copy(unique_id)
+        check("pmc_slab_init", lib().pmc_slab_init(self._h, rank, world, uid))
+
+    def slab_exchange(self) -> None:
+        check("pmc_slab_exchange", lib().pmc_slab_exchange(self._h))
+
+    def slab_sweep(self, s: int) -> None:
+        check("pmc_slab_sweep", lib().pmc_slab_sweep(self._h, s))
+
+    def slab_finish(self) -> None:
+        check("pmc_slab_finish", lib().pmc_slab_finish(self._h))
+
+    def slab_timing(self, enable: bool) -> dict:
+        a, b = C.c_double(), C.c_double()
+        na, nb = C.c_int(), C.c_int()
+        check("pmc_slab_timing", lib().pmc_slab_timing(self._h, int(enable), C.byref(a), C.byref(na), C.byref(b),
+                                                       C.byref(nb)))
+        return {"subsweep_ms": a.value, "n_subsweep": na.value, "shift_ms": b.value, "n_shift": nb.value}
+
     def shift(self, s: int) -> None:
         check("pmc_shift", lib().pmc_shift(self._h, s))
 
@@ -226,6 +253,13 @@ class PmcContext:
         check("pmc_plane_span", lib().pmc_plane_span(self._h, z_local, C.byref(a), C.byref(b), C.byref(c),
                                                      C.byref(d)))
         return a.value, b.value, c.value, d.value
+
+
+def comm_unique_id() -> bytes:
+    """A fresh RCCL unique id (rank 0 of a slab run broadcasts it)."""
+    buf = (C.c_ubyte * 128)()
+    check("pmc_comm_unique_id", lib().pmc_comm_unique_id(buf))
+    return bytes(buf)
 
 
 def selftest_detmath(words: np.ndarray):

@@ -21,6 +21,7 @@ tests drive the same class with the C oracle and the gloo backend.
 from __future__ import annotations
 
 from dataclasses import dataclass
+import os
 from typing import Callable, List, Optional, Tuple
 
 from .plan import sweep_plan
@@ -54,17 +55,20 @@ class SlabGeometry:
 class TorchP2P:
     """Halo transport over torch.distributed point-to-point (nccl/RCCL or gloo)."""
 
-    def __init__(self, rank: int, world: int, group=None):
+    def __init__(self, rank: int, world: int, group=None, self_p2p: bool = False):
         self.rank = rank
         self.world = world
         self.group = group
+        # world == 1 normally copies locally; self_p2p sends to itself through torch.distributed
+        # (a one-rank RCCL group: the multi-GPU transport path, rehearsed on one GPU)
+        self.self_p2p = self_p2p
 
     def start(self, sends: List[Tuple[object, int]], recvs: List[Tuple[object, int]]):
         """Issue the exchange; returns a handle for wait().  sends/recvs: (tensor, peer).  Every rank
         issues its sends and receives in the same logical order (down-plane first, then up-plane),
         which fixes the pairwise matching."""
         import torch.distributed as dist
-        if self.world == 1:
+        if self.world == 1 and not self.self_p2p:
             # periodic single-rank slab: each receive takes the send with the same role
             for (dst, _), (src, _) in zip(recvs, sends_for_self(sends, recvs)):
                 dst.copy_(src)
@@ -130,6 +134,7 @@ class SlabSimulation:
         ctx.attach_state(disk[0], n[0], disk[1], n[1])
         sim = cls(ctx, g, disk, n, TorchP2P(rank, world, group), seed=seed)
         sim.stream = stream
+        sim.bstream = torch.cuda.Stream()  # boundary planes, concurrent with the interior
         if world > 1:
             import torch.distributed as dist
             dist.barrier(group=group)      # a collective first, then point-to-point (NCCL rule)
@@ -154,40 +159,82 @@ class SlabSimulation:
         # counts travel as bytes: NCCL/RCCL has no 16-bit integer type
         return d, self.n[self.cur][z_local + 1].view(torch.uint8)
 
-    def _exchange(self, send_down: bool, send_up: bool, with_n: bool, wait: bool = True):
+    @staticmethod
+    def _colour_cells(plane, colour: int):
+        """The cells of `colour` (x % 2 == ox, y % 2 == oy; itoa, start.cu:153-157) of one plane
+        (cps_y, cps_x, 3, nmax), as a strided view: the only cells a phase changes."""
+        ox, oy = (colour // 4) % 2, (colour // 2) % 2
+        cy, cx = plane.shape[0], plane.shape[1]
+        return plane.reshape(cy // 2, 2, cx // 2, 2, -1)[:, oy, :, ox]
+
+    def _buf(self, key, like):
+        """Persistent contiguous staging buffer for a packed colour plane (per role)."""
+        bufs = self.__dict__.setdefault("_bufs", {})
+        b = bufs.get(key)
+        if b is None or b.shape != like.shape or b.device != like.device:
+            import torch
+            b = bufs[key] = torch.empty(like.shape, dtype=like.dtype, device=like.device)
+        return b
+
+    def _exchange(self, send_down: bool, send_up: bool, with_n: bool, wait: bool = True, stream=None,
+                  colour=None):
+        """Send the boundary plane(s), receive the halo(s).  With `colour` (a phase exchange) only
+        that colour's quarter of the plane travels: packed into a staging buffer on the current
+        stream, unpacked into the halo when the exchange is completed (_complete)."""
         g = self.g
-        sends, recvs = [], []
-        if send_down:   # my plane 0 -> top halo of the rank below; my top halo <- plane 0 of above
-            d, nn = self._plane(0, with_n)
-            sends.append((d, g.below))
-            rd, rn = self._plane(g.nz, with_n)
-            recvs.append((rd, g.above))
+        sends, recvs, unpack = [], [], []
+        local = self.tp.world == 1 and not getattr(self.tp, "self_p2p", False)
+
+        def add(src_z, dst_z, peer_to, peer_from, role):
+            d, nn = self._plane(src_z, with_n)
+            rd, rn = self._plane(dst_z, with_n)
+            if colour is not None:
+                sv, rv = self._colour_cells(d, colour), self._colour_cells(rd, colour)
+                if local:                       # periodic single rank: one strided copy
+                    unpack.append((rv, sv))
+                    return
+                sb = self._buf(("s", role), sv)
+                sb.copy_(sv)
+                rb = self._buf(("r", role), rv)
+                sends.append((sb, peer_to))
+                recvs.append((rb, peer_from))
+                unpack.append((rv, rb))
+                return
+            sends.append((d, peer_to))
+            recvs.append((rd, peer_from))
             if with_n:
-                sends.append((nn, g.below))
-                recvs.append((rn, g.above))
-        if send_up:     # my plane nz-1 -> bottom halo of the rank above; my bottom halo <- below
-            d, nn = self._plane(g.nz - 1, with_n)
-            sends.append((d, g.above))
-            rd, rn = self._plane(-1, with_n)
-            recvs.append((rd, g.below))
-            if with_n:
-                sends.append((nn, g.above))
-                recvs.append((rn, g.below))
-        with self._on_stream():
-            handle = self.tp.start(sends, recvs)
+                sends.append((nn, peer_to))
+                recvs.append((rn, peer_from))
+
+        with self._on_stream(stream):
+            if send_down:   # my plane 0 -> top halo of the rank below; my top halo <- plane 0 of above
+                add(0, g.nz, g.below, g.above, "down")
+            if send_up:     # my plane nz-1 -> bottom halo of the rank above; my bottom halo <- below
+                add(g.nz - 1, -1, g.above, g.below, "up")
+            works = self.tp.start(sends, recvs) if sends else []
+            handle = (works, unpack)
             if wait:
-                self.tp.wait(handle)
+                self._complete(handle)
                 return None
         return handle
+
+    def _complete(self, handle) -> None:
+        """Finish an exchange on the current stream: wait for the transport, unpack the halos."""
+        if not handle:
+            return
+        works, unpack = handle
+        self.tp.wait(works)
+        for dst, src in unpack:
+            dst.copy_(src)
 
     def _wait(self, handle) -> None:
         if handle:
             with self._on_stream():
-                self.tp.wait(handle)
+                self._complete(handle)
 
-    def _on_stream(self):
+    def _on_stream(self, stream=None):
         import contextlib
-        stream = getattr(self, "stream", None)
+        stream = stream if stream is not None else getattr(self, "stream", None)
         if stream is None:
             return contextlib.nullcontext()
         import torch
@@ -195,7 +242,7 @@ class SlabSimulation:
 
     def exchange_after_phase(self, colour: int) -> None:
         oz = colour % 2          # itoa (start.cu:153-157): offset[2] = colour % 2
-        self._exchange(send_down=(oz == 0), send_up=(oz == 1), with_n=False)
+        self._exchange(send_down=(oz == 0), send_up=(oz == 1), with_n=False, colour=colour)
 
     def exchange_after_shift(self) -> None:
         self._exchange(True, True, with_n=True)
@@ -212,6 +259,60 @@ class SlabSimulation:
         self.cur ^= 1
 
     def sweep(self, s: int, timer=None) -> None:
+        if getattr(self, "bstream", None) is not None and hasattr(self.engine, "phase_range_on"):
+            return self._sweep_two_streams(s, timer)
+        return self._sweep_one_stream(s, timer)
+
+    def _sweep_two_streams(self, s: int, timer=None) -> None:
+        """One sweep, boundary planes on a second stream beside the interior (GPU path).
+
+        Per colour k, with S the context stream and T the boundary stream:
+          S: wait B(k-1) -> interior I(k) (planes [1, nz-1): no halo read) -> record I(k)
+          T: wait I(k-1) and the halo exchange of k-1 -> boundary B(k) (planes 0 and nz-1)
+             -> record B(k) -> start the exchange of k (the NCCL stream waits on T)
+        so I(k) and B(k) run together, and the exchange of k overlaps I(k+1).  I(k) never touches
+        the boundary planes an exchange sends nor the halos it receives; B(k) waits for the
+        exchange of k-1 to complete (send and receive).  Cells of one colour are independent, so
+        the result equals the sequential schedule bit for bit.  shiftCells (S) waits for both
+        streams and the last exchange; its own exchange overlaps the next sweep's first interior.
+        `timer(kind, fn, stream)` wraps each launch.
+        """
+        import torch
+        run = timer or (lambda kind, fn, stream=None: fn())
+        nz = self.g.nz
+        S, T = self.stream, self.bstream
+        order, _, _ = self.plan_fn(self.seed, s, self.w)
+        pending = getattr(self, "_pending", None)
+        ev_b = None
+        ev_i = torch.cuda.Event()        # "I(-1)": everything issued on S before this sweep
+        ev_i.record(S)
+        for colour in order:
+            if ev_b is not None:
+                S.wait_event(ev_b)
+            if nz > 2:
+                run("phase", lambda: self.engine.phase_range(colour, s, 1, nz - 1), S)
+            ev_prev_i = ev_i
+            ev_i = torch.cuda.Event()
+            ev_i.record(S)
+            with torch.cuda.stream(T):
+                T.wait_event(ev_prev_i)
+                self._complete(pending)
+                run("phase", lambda: self.engine.phase_range_on(colour, s, 0, 1, T.cuda_stream), T)
+                if nz > 1:
+                    run("phase", lambda: self.engine.phase_range_on(colour, s, nz - 1, nz, T.cuda_stream), T)
+                ev_b = torch.cuda.Event()
+                ev_b.record(T)
+                oz = colour % 2
+                pending = self._exchange(send_down=(oz == 0), send_up=(oz == 1), with_n=False, wait=False,
+                                         stream=T, colour=colour)
+        S.wait_event(ev_i)
+        S.wait_event(ev_b)
+        self._wait(pending)
+        run("shift", lambda: self.engine.shift(s), S)
+        self.cur ^= 1
+        self._pending = self._exchange(True, True, with_n=True, wait=False)
+
+    def _sweep_one_stream(self, s: int, timer=None) -> None:
         """One sweep with communication hidden behind the halo-free interior.
 
         Per colour: (1) the interior planes [1, nz-1) -- they read no halo -- run while the
@@ -232,7 +333,8 @@ class SlabSimulation:
             if nz > 1:
                 run("phase", lambda: self.engine.phase_range(colour, s, nz - 1, nz))
             oz = colour % 2
-            pending = self._exchange(send_down=(oz == 0), send_up=(oz == 1), with_n=False, wait=False)
+            pending = self._exchange(send_down=(oz == 0), send_up=(oz == 1), with_n=False, wait=False,
+                                     colour=colour)
         self._wait(pending)
         run("shift", lambda: self.engine.shift(s))
         self.cur ^= 1
@@ -266,3 +368,84 @@ class SlabSimulation:
     def owned(self):
         """(disk, n) of the owned planes of the current buffer."""
         return self.disk[self.cur][1:-1], self.n[self.cur][1:-1]
+
+
+def _rccl_lib_path() -> Optional[str]:
+    """The librccl torch already loaded (same soname: dlopen in C shares that instance)."""
+    import torch
+    cand = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    return cand if os.path.exists(cand) else None
+
+
+class SlabDriver:
+    """The product multi-GPU path: the C slab driver (pmc_slab_*), one process per GPU.
+
+    The sweep schedule (interior on the context stream, each colour's boundary plane on an
+    auxiliary stream beside it, colour-packed RCCL send/recv of the boundary cells) runs in C, so
+    the host issues a sweep in a few dozen HIP/RCCL calls.  SlabSimulation above is the same
+    schedule in Python over torch.distributed; the CPU tests drive it with the oracle and gloo.
+    """
+
+    def __init__(self, cps: int, nz_local: int, rank: int, world: int, stream=None, atoms_per_rank: int = 0,
+                 atoms_total: int = 0, nmax: int = 16, n_moves: int = 10, seed: int = 1234,
+                 use_rccl: Optional[bool] = None, group=None):
+        import torch
+        from .engine import PmcContext, comm_unique_id
+        self.g = SlabGeometry(cps, nz_local, rank, world, nmax)
+        if stream is None:
+            stream = torch.cuda.Stream()
+        self.stream = stream
+        self.ctx = PmcContext(cps, cps_z=self.g.cps_z, nz_local=nz_local, z0=self.g.z0, halo=1, nmax=nmax,
+                              n_moves=n_moves, seed=seed, stream=stream.cuda_stream)
+        use_rccl = world > 1 if use_rccl is None else use_rccl
+        uid = None
+        if use_rccl:
+            lib_path = _rccl_lib_path()
+            if lib_path and not os.environ.get("PMC_RCCL_LIB"):
+                os.environ["PMC_RCCL_LIB"] = lib_path
+            buf = torch.zeros(128, dtype=torch.uint8)
+            if rank == 0:
+                buf = torch.tensor(list(comm_unique_id()), dtype=torch.uint8)
+            if world > 1:
+                import torch.distributed as dist
+                on = buf.cuda() if dist.get_backend(group) == "nccl" else buf
+                dist.broadcast(on, src=0, group=group)
+                buf = on.cpu()
+            uid = bytes(buf.numpy().tobytes())
+        self.ctx.slab_init(rank, world, uid)      # RCCL communicator: collective over the ranks
+        if atoms_total:
+            self.ctx.init_lattice_global(atoms_total)
+            self.ctx.slab_exchange()
+        elif atoms_per_rank:
+            self.ctx.init_lattice(atoms_per_rank)
+            self.ctx.slab_exchange()
+
+    def sweep(self, s: int) -> None:
+        self.ctx.slab_sweep(s)
+
+    def finish(self) -> None:
+        self.ctx.slab_finish()
+
+    def run(self, first: int, count: int) -> None:
+        for k in range(count):
+            self.sweep(first + k)
+        self.finish()
+
+    def load_state(self, disk, n) -> None:
+        """Owned planes from host arrays ((nz, cps, cps, 3, nmax) floats, (nz, cps, cps) int16);
+        halos refilled from the neighbours."""
+        import numpy as np
+        full_d, full_n = self.ctx.copy_out()
+        plane = self.g.cps * self.g.cps
+        row = 3 * self.g.nmax
+        full_d[plane * row:(self.g.nz + 1) * plane * row] = np.asarray(disk, np.float32).reshape(-1)
+        full_n[plane:(self.g.nz + 1) * plane] = np.asarray(n, np.int16).reshape(-1)
+        self.ctx.copy_in(full_d, full_n)
+        self.ctx.slab_exchange()
+
+    def owned(self):
+        """(disk, n) of the owned planes as host arrays (after finish())."""
+        d, n = self.ctx.copy_out()
+        plane = self.g.cps * self.g.cps
+        row = 3 * self.g.nmax
+        return d[plane * row:(self.g.nz + 1) * plane * row], n[plane:(self.g.nz + 1) * plane]

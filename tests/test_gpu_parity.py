@@ -233,14 +233,18 @@ print("ok", r["accepted"])
     assert out.stdout.startswith("ok")
 
 
-def test_gpu_slab_single_rank_equals_whole_box(pmc):
+@pytest.mark.parametrize("nz,atoms,two_streams", [(16, 10_000, True), (16, 10_000, False), (4, 2_500, True)])
+def test_gpu_slab_single_rank_equals_whole_box(pmc, nz, atoms, two_streams):
     """The HIP slab path (halo planes, global z images, plane exchange through torch tensors)
-    with one rank reproduces the whole-box run bit for bit."""
+    with one rank reproduces the whole-box run bit for bit -- with the boundary planes on their
+    own stream beside the interior (the multi-GPU schedule) and with the one-stream schedule."""
     import torch
     from pmc_amd.slab import SlabSimulation
-    sim = SlabSimulation.create(cps=16, nz_local=16, rank=0, world=1, atoms_per_rank=10_000)
-    whole = pmc.PmcContext(16)
-    whole.init_lattice(10_000)
+    sim = SlabSimulation.create(cps=16, nz_local=nz, rank=0, world=1, atoms_per_rank=atoms)
+    if not two_streams:
+        sim.bstream = None
+    whole = pmc.PmcContext(16, cps_z=nz)
+    whole.init_lattice(atoms)
     sim.run(0, 4)
     for s in range(4):
         whole.sweep(s)
@@ -251,6 +255,8 @@ def test_gpu_slab_single_rank_equals_whole_box(pmc):
     import pmc_oracle
     assert pmc_oracle.valid_slots_equal(d_slab.cpu().numpy().reshape(-1), n, disk, n, 16)
     assert sim.ctx.stats() == whole.stats()
+    if nz != 16:
+        return
     # energies: slab pairs across the (self-)boundary count half on each side -> same total
     assert sim.ctx.energy() == pytest.approx(whole.energy(), rel=1e-12, abs=1e-9)
 
@@ -277,3 +283,52 @@ def test_gpu_init_lattice_global_slab_planes(pmc, oracle):
                                         dw[ref.start * row:ref.stop * row], nw[ref], 16)
         total += int(n[own].sum())
     assert total == atoms
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nz,atoms,rccl", [(16, 10_000, False), (16, 10_000, True), (4, 2_500, True)])
+def test_gpu_c_slab_driver_equals_whole_box(pmc, oracle, nz, atoms, rccl):
+    """The C slab driver (pmc_slab_*: two streams, colour-packed halo exchange; with rccl=True
+    through a one-rank RCCL communicator sending to itself, the multi-GPU transport path) equals
+    the whole-box run bit for bit: every occupied slot, counts, counters and the energy."""
+    import torch
+    from pmc_amd.slab import SlabDriver
+    drv = SlabDriver(cps=16, nz_local=nz, rank=0, world=1, atoms_per_rank=atoms, use_rccl=rccl)
+    whole = pmc.PmcContext(16, cps_z=nz)
+    whole.init_lattice(atoms)
+    drv.run(0, 4)
+    for s in range(4):
+        whole.sweep(s)
+    torch.cuda.synchronize()
+    d_slab, n_slab = drv.owned()
+    disk, n = whole.copy_out()
+    assert np.array_equal(n_slab, n)
+    assert oracle.valid_slots_equal(d_slab, n_slab, disk, n, 16)
+    assert drv.ctx.stats() == whole.stats()
+    assert drv.ctx.error_flags() == 0
+    assert drv.ctx.energy() == pytest.approx(whole.energy(), rel=1e-12, abs=1e-9)
+
+
+@pytest.mark.gpu
+def test_gpu_c_slab_driver_timing_and_restart(pmc, oracle, tmp_path):
+    """Per-launch HIP-event timing of the C driver, and snapshot + halo refill: 2 sweeps, save,
+    2 more; a fresh driver restored from the snapshot repeats the last 2 bit for bit."""
+    from pmc_amd.slab import SlabDriver
+    drv = SlabDriver(cps=16, nz_local=16, rank=0, world=1, atoms_per_rank=10_000)
+    drv.ctx.slab_timing(True)
+    drv.run(0, 2)
+    t = drv.ctx.slab_timing(False)
+    assert t["n_subsweep"] == 2 * 16 and t["n_shift"] == 2 and t["subsweep_ms"] > 0 and t["shift_ms"] > 0
+    path = str(tmp_path / "slab.pmcsnap")
+    drv.ctx.save_snapshot(path, 2)
+    drv.run(2, 2)
+    d1, n1 = drv.owned()
+    s1 = drv.ctx.stats()
+    drv2 = SlabDriver(cps=16, nz_local=16, rank=0, world=1)
+    first = drv2.ctx.load_snapshot(path)
+    drv2.ctx.slab_exchange()
+    drv2.run(first, 2)
+    d2, n2 = drv2.owned()
+    assert np.array_equal(n1, n2)
+    assert oracle.valid_slots_equal(d1, n1, d2, n2, 16)
+    assert drv2.ctx.stats() == s1

@@ -1,0 +1,144 @@
+"""Strong-scaling rehearsal on ONE GPU: time the per-rank work of an R-rank config-4 run.
+
+  python tools/strong_emulation.py [--ranks 8] [--cps 128] [--atoms 10000000] [--p2p rccl|local]
+
+An R-rank strong-scaling run (bench.py --strong) gives every rank cps/R planes of the 128^3 box
+plus two halo planes.  Here one process holds such a slab -- the bottom cps/R planes of the
+config-3 lattice (the lattice period divides the slab: 16 planes = 40 = 27 lattice spacings at
+1e7 particles, so the slab is periodic in z without a seam) -- and runs the product slab driver
+(SlabSimulation: interior and boundary streams, colour-packed halo exchange) on it.  With
+--p2p rccl the halos travel through a one-rank RCCL group (send/recv to itself: the RCCL kernels
+and the torch.distributed host path of the multi-GPU run); --p2p local copies them.
+
+Prints one JSON line: the full-box sweep time T1 (pmc_phase/pmc_shift, as bench.py at N=1), the
+emulated rank's sweep time TR, and the compute-side projection T1 / TR of the R-GPU speedup.  It
+does not see xGMI link time or waits on slower neighbours: a rehearsal, not a measurement of N GPUs.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "parallel-monte-carlo_amd"))
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ranks", type=int, default=8)
+    ap.add_argument("--cps", type=int, default=128)
+    ap.add_argument("--atoms", type=int, default=10_000_000)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--p2p", choices=["rccl", "local"], default="rccl")
+    ap.add_argument("--driver", choices=["c", "python"], default="c",
+                    help="c: the C slab driver (pmc_slab_*, product); python: SlabSimulation")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import pmc_amd
+    from pmc_amd.plan import sweep_plan
+    from pmc_amd.slab import SlabSimulation, TorchP2P
+
+    cps, R = args.cps, args.ranks
+    nz = cps // R
+    assert cps % R == 0 and nz % 2 == 0 and nz >= 4, "slab thickness must be even and >= 4"
+    torch.cuda.set_device(0)
+    stream = torch.cuda.Stream()
+
+    # ---- full box: the N=1 reference time (bench.py's non-slab path) ------------------------
+    full = pmc_amd.PmcContext(cps, stream=stream.cuda_stream)
+    full.init_lattice(args.atoms)
+    disk_h, n_h = full.copy_out()
+
+    def full_sweep(s):
+        for colour in sweep_plan(1234, s, 2.5)[0]:
+            full.phase(colour, s)
+        full.shift(s)
+
+    for s in range(args.warmup):
+        full_sweep(s)
+    full.synchronize()
+    full.stats(reset=True)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        full_sweep(args.warmup + k)
+    full.synchronize()
+    t1 = (time.perf_counter() - t0) / args.steps
+    trials_full = full.stats()["trials"] / args.steps
+    # the slab: the first nz planes of the lattice state, z moved into the thin box's frame
+    nmax = full.nmax
+    plane = cps * cps
+    d = disk_h.reshape(-1, 3, nmax)[: plane * nz].copy()
+    n = n_h[: plane * nz].copy()
+    shift_z = np.float32(cps * 2.5 / 2 - nz * 2.5 / 2)
+    for k in range(nmax):
+        occ = n > k
+        d[occ, 2, k] = d[occ, 2, k] + shift_z
+    full.close()
+
+    # ---- one emulated rank ------------------------------------------------------------------
+    py = args.driver == "python"
+    if args.p2p == "rccl" and py:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    if py:
+        sim = SlabSimulation.create(cps=cps, nz_local=nz, rank=0, world=1, stream=stream)
+        sim.tp = TorchP2P(0, 1, self_p2p=args.p2p == "rccl")
+        with torch.cuda.stream(stream):
+            sim.disk[0][1:nz + 1].copy_(torch.from_numpy(d).view(nz, cps, cps, 3, nmax))
+            sim.n[0][1:nz + 1].copy_(torch.from_numpy(n).view(nz, cps, cps))
+        torch.cuda.synchronize()
+        sim.exchange_full()
+    else:
+        from pmc_amd.slab import SlabDriver
+        sim = SlabDriver(cps=cps, nz_local=nz, rank=0, world=1, stream=stream, use_rccl=args.p2p == "rccl")
+        sim.load_state(d, n)
+    for s in range(args.warmup):
+        sim.sweep(s)
+    sim.finish()
+    torch.cuda.synchronize()
+    sim.ctx.stats(reset=True)
+    t0 = time.perf_counter()
+    issue = 0.0
+    for k in range(args.steps):
+        ti = time.perf_counter()
+        sim.sweep(args.warmup + k)
+        issue += time.perf_counter() - ti
+    sim.finish()
+    torch.cuda.synchronize()
+    tr = (time.perf_counter() - t0) / args.steps
+    trials_rank = sim.ctx.stats()["trials"] / args.steps
+    # the same sweeps issued with the GPU idle-free: host time per sweep when it never waits
+    with torch.cuda.stream(stream):
+        torch.cuda._sleep(int(2e9))      # ~1 s of GPU spin so the host runs ahead unblocked
+    ti = time.perf_counter()
+    for k in range(3):
+        sim.sweep(args.warmup + args.steps + k)
+    host_only = (time.perf_counter() - ti) / 3
+    sim.finish()
+    torch.cuda.synchronize()
+    flags = sim.ctx.error_flags()
+    out = {"tool": "strong_emulation", "ranks_emulated": R, "planes_per_rank": nz, "p2p": args.p2p,
+           "driver": args.driver,
+           "full_box_sweep_ms": t1 * 1e3, "full_box_trial_moves_per_s": trials_full / t1,
+           "rank_sweep_ms": tr * 1e3, "rank_trial_moves_per_s": trials_rank / tr,
+           "projected_speedup": t1 / tr, "projected_efficiency": t1 / tr / R,
+           "projected_whole_job_trial_moves_per_s": trials_rank * R / tr,
+           "host_issue_ms_per_sweep": issue / args.steps * 1e3, "host_only_ms_per_sweep": host_only * 1e3,
+           "error_flags": flags,
+           "note": "one GPU running one rank's slab of the config-4 box with the product slab driver; "
+                   "excludes xGMI link time and neighbour skew"}
+    print(json.dumps(out))
+    if args.p2p == "rccl" and py:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
