@@ -217,6 +217,7 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     const int nm = NMC > 0 ? NMC : g.nmax;        // compile-time for the common nmax
     const int lcap = LCAP > 0 ? LCAP : lcap_rt;            // layout capacity (>= cap)
     const int stride = subsweep_stride(lcap);              // compile-time -> LDS offset immediates
+    const int lcap4 = (lcap + 3) & ~3;                     // per-move randoms at rows' tails (16 B aligned)
     float* py_ = px_ + stride;
     float* pz_ = py_ + stride;
     float* buf = pz_ + stride;                  // term list: signed r2 values
@@ -310,6 +311,15 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
         G0 = (R * cs) * g.sigma;   // lanes 0-15: g0*sigma of move m0+lane; 32-47: g2*sigma
         G1 = (R * sn) * g.sigma;   // lanes 0-15: g1*sigma
         TT = -lg;         // lanes 16-31: acceptance threshold of move m0+lane-16
+        // park move j's randoms in the unused tails of the y / z rows (slots [lcap4, lcap4 + 32):
+        // never staged, read by the moves only as "far" partners' don't-care values): (d0, d1) at
+        // y-tail pair j, (d2, T) at z-tail pair j.  A move then takes them with two broadcast LDS
+        // reads off one address instead of four v_readlane.
+        {
+            const int j = lane & 15;
+            if (lane < 16) *(float2*)(py_ + lcap4 + 2 * j) = make_float2(G0, G1);
+            else if (lane < 48) pz_[lcap4 + 2 * j + (lane < 32 ? 1 : 0)] = lane < 32 ? TT : G0;
+        }
     };
     rng_chunk(0, true);
     PMC_STAMP(3);
@@ -449,14 +459,18 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     int n_acc = 0, n_ev = 0;
     int i = 0;
     // ---- 4. trial moves --------------------------------------------------------------------
+    // The number of 64-partner blocks per move is fixed for the visit: the move loop is
+    // instantiated per block count (1-4 at the main capacity), so each move runs straight-line
+    // block code with no per-move loop or bound tests (the full-capacity launches keep the loop).
+    auto move_loop = [&](auto nb_c) {
+    constexpr int NB = decltype(nb_c)::value;
     for (int m0 = 0; m0 < g.n_moves; m0 += 16) {
         if (m0 > 0) rng_chunk(m0, false);
-        const int mend = (g.n_moves - m0) < 16 ? (g.n_moves - m0) : 16;
+        const int mend = wave_uniform((g.n_moves - m0) < 16 ? (g.n_moves - m0) : 16);
         for (int ml = 0; ml < mend; ++ml) {
-            const float d0 = as_f(__builtin_amdgcn_readlane(as_i(G0), ml));
-            const float d1 = as_f(__builtin_amdgcn_readlane(as_i(G1), ml));
-            const float d2 = as_f(__builtin_amdgcn_readlane(as_i(G0), 32 + ml));
-            const float Tm = as_f(__builtin_amdgcn_readlane(as_i(TT), 16 + ml));
+            const float2 mva = *(const float2*)(py_ + lcap4 + 2 * ml);
+            const float2 mvb = *(const float2*)(pz_ + lcap4 + 2 * ml);
+            const float d0 = mva.x, d1 = mva.y, d2 = mvb.x, Tm = mvb.y;
             const int si = S_nb + i;
             const float xi = px_[si], yi = py_[si], zi = pz_[si];
             const float qx = xi + d0;                  // make_move: x + g * sigma
@@ -491,14 +505,36 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
                     if (__builtin_amdgcn_inverse_ballot_w64(mo)) buf[mbcnt64_add(mo, cn)] = r2on;
                     C = cn + __popcll(mo);
                 };
-                block(0);
-                if (K > kWave) {
-                    block(kWave);
-                    for (int base = 2 * kWave; base < K; base += kWave) block(base);
+                if constexpr (NB > 0) {
+#pragma unroll
+                    for (int b = 0; b < NB; ++b) block(b * kWave);
+                } else {
+                    block(0);
+                    for (int base = kWave; base < K; base += kWave) block(base);
                 }
                 // 4b. energies of the listed terms: term t on lane t % 64, ascending t.  The 64
                 // slots after the list get kPad (r2 = 1e30: inv^3 underflows to +0, so the term
                 // is exactly +0 and adding it leaves a lane's sum unchanged) -- no lane mask.
+#if defined(PMC_PAD_VALU) || defined(PMC_PAD_SALU) || defined(PMC_PAD_LDS)
+                {   // analysis builds only: marginal cost of extra independent instructions per move
+                    float pv = (float)lane;
+                    int ps = C;
+#ifdef PMC_PAD_VALU
+#pragma unroll
+                    for (int q = 0; q < PMC_PAD_VALU; ++q) asm volatile("v_add_f32 %0, 1.0, %0" : "+v"(pv));
+#endif
+#ifdef PMC_PAD_SALU
+#pragma unroll
+                    for (int q = 0; q < PMC_PAD_SALU; ++q) asm volatile("s_add_u32 %0, %0, 3" : "+s"(ps) :: "scc");
+#endif
+#ifdef PMC_PAD_LDS
+#pragma unroll
+                    for (int q = 0; q < PMC_PAD_LDS; ++q) asm volatile("ds_read_b32 %0, %1 offset:4" : "=v"(pv) : "v"(0));
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+                    asm volatile("" :: "v"(pv), "s"(ps));
+                }
+#endif
                 buf[C + lane] = kPad;
                 float acc = 0.0f;
                 for (int t0 = 0; t0 < C; t0 += kWave) acc = acc + lj4_signed_max(buf[t0 + lane], r2min);
@@ -517,6 +553,16 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
             i += 1;
             if (i >= n_own) i = 0;
         }
+    }
+    };
+    if constexpr (LCAP == kMainCap) {
+        const int nb = (K + kWave - 1) / kWave;                 // 1..4 (K <= cap <= 224)
+        if (nb <= 1) move_loop(std::integral_constant<int, 1>{});
+        else if (nb == 2) move_loop(std::integral_constant<int, 2>{});
+        else if (nb == 3) move_loop(std::integral_constant<int, 3>{});
+        else move_loop(std::integral_constant<int, 4>{});
+    } else {
+        move_loop(std::integral_constant<int, 0>{});
     }
 
     PMC_STAMP(8);
@@ -906,6 +952,9 @@ __global__ void k_selftest(const uint32_t* __restrict__ words, int count, float*
 // ------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------
+#ifndef PMC_FALLBACK_BLOCKS
+#define PMC_FALLBACK_BLOCKS 64   // fixed grid of the overflow launch (it strides over the queue)
+#endif
 int subsweep_capacity(const DevGeom& g) {
     // Partners per wave held in LDS by the main launch.  Sized so a wave needs at most 5 KiB of
     // LDS (-> 32 waves/CU, the hardware limit): 3 floats per partner (x, y, z) + 2 term-list
@@ -934,7 +983,7 @@ static void launch_subsweep_t(const DevGeom& g, float* disk, const int16_t* n, i
                        disk, n, ox, oy, oz, sweep, stats, cap, ovf, cz0, ncz);
     if (cap < full) {
         const size_t lds_full = sizeof(float) * (size_t)lds_floats_per_wave(full) * kSubWaves;
-        hipLaunchKernelGGL((k_subsweep_fallback<NSLOT, NMC, OFF32>), dim3(64), dim3(kWave * kSubWaves), lds_full, st,
+        hipLaunchKernelGGL((k_subsweep_fallback<NSLOT, NMC, OFF32>), dim3(PMC_FALLBACK_BLOCKS), dim3(kWave * kSubWaves), lds_full, st,
                            g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0);
     }
 }

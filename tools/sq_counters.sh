@@ -14,7 +14,7 @@ import csv, glob, sys, collections
 agg = collections.defaultdict(list)
 for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if r["Kernel_Name"].startswith("k_subsweep<") or r["Kernel_Name"].startswith("k_subsweep("):
+        if r["Kernel_Name"].split("(")[0].split("<")[0] == "k_subsweep":
             agg[(r["Dispatch_Id"], r["Counter_Name"])].append(float(r["Counter_Value"]))
 per = collections.defaultdict(list)
 for (d, c), v in agg.items():
