@@ -467,9 +467,10 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     for (int m0 = 0; m0 < g.n_moves; m0 += 16) {
         if (m0 > 0) rng_chunk(m0, false);
         const int mend = wave_uniform((g.n_moves - m0) < 16 ? (g.n_moves - m0) : 16);
-        for (int ml = 0; ml < mend; ++ml) {
-            const float2 mva = *(const float2*)(py_ + lcap4 + 2 * ml);
-            const float2 mvb = *(const float2*)(pz_ + lcap4 + 2 * ml);
+        const float* mvp = py_ + lcap4;                    // this chunk's move randoms (y tail)
+        for (int ml = 0; ml < mend; ++ml, mvp += 2) {
+            const float2 mva = *(const float2*)mvp;            // (d0, d1)
+            const float2 mvb = *(const float2*)(mvp + stride); // (d2, T) in the z tail
             const float d0 = mva.x, d1 = mva.y, d2 = mvb.x, Tm = mvb.y;
             const int si = S_nb + i;
             const float xi = px_[si], yi = py_[si], zi = pz_[si];
@@ -536,8 +537,9 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
                 }
 #endif
                 buf[C + lane] = kPad;
-                float acc = 0.0f;
-                for (int t0 = 0; t0 < C; t0 += kWave) acc = acc + lj4_signed_max(buf[t0 + lane], r2min);
+                // the first pass unconditionally (C == 0 reads only kPad: +0), the rest looped
+                float acc = 0.0f + lj4_signed_max(buf[lane], r2min);
+                for (int t0 = kWave; t0 < C; t0 += kWave) acc = acc + lj4_signed_max(buf[t0 + lane], r2min);
                 // quarter energies were accumulated; the factor 4 is exact, so 4*(sum of u)
                 // equals the sum of the 4u the oracle accumulates, bit for bit
                 const float dEu = wave_sum_fixed_order_s(4.0f * acc);   // SGPR
