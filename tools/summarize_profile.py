@@ -5,8 +5,9 @@
 Writes
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (copied verbatim)
   profiles/<tag>_pmc.txt            per-kernel mean of every collected counter
-  profiles/pmc_traffic.json         HBM bytes per k_subsweep launch from FETCH_SIZE / WRITE_SIZE
-                                    (read by bench.py for roofline.traffic)
+  profiles/<tag>_fetch_write_size.json   FETCH_SIZE / WRITE_SIZE per k_subsweep launch (a cross-check:
+                                    bench.py's roofline.traffic comes from profiles/pmc_traffic.json,
+                                    written from tools/tcc_traffic.sh's TCC_EA0 request counts)
 
 FETCH_SIZE and WRITE_SIZE are in KiB per dispatch and come from separate passes (they cannot share
 one on gfx950).  MI355X_MICROARCH.md: FETCH_SIZE reads exactly half the bytes of a 16-B-per-lane
@@ -62,7 +63,7 @@ def main():
             "note": "rocprofv3 FETCH_SIZE+WRITE_SIZE (KiB x 1024), separate passes; raw, the gfx950 x2 "
                     "FETCH correction is calibrated only for 16-B/lane streams (upper estimate given)",
         }
-        with open(os.path.join(out, "pmc_traffic.json"), "w") as f:
+        with open(os.path.join(out, f"{tag}_fetch_write_size.json"), "w") as f:
             json.dump(traffic, f, indent=1)
         print(json.dumps(traffic))
     print("\n".join(lines))
