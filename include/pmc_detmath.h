@@ -65,7 +65,7 @@ PMC_HD pmc_u32x4 pmc_philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32
 /* Counter-slot tags (SURVEY Appendix A "RNG slots"). Counter = (idx, cell_id, sweep, tag). */
 #define PMC_TAG_MOVE    0u  /* idx = move m: 4 words -> 3 normals (two Box-Muller pairs)     */
 #define PMC_TAG_ACCEPT  1u  /* idx = move m: word 0 -> exponential acceptance threshold      */
-#define PMC_TAG_SHUFFLE 2u  /* idx = slot i: word 0 -> Fisher-Yates index in [0, i]         */
+#define PMC_TAG_SHUFFLE 2u  /* idx = i >> 2: word i & 3 -> Fisher-Yates index of slot i in [0, i] */
 #define PMC_TAG_PLAN    3u  /* host sweep plan, cell_id = 0xFFFFFFFF                          */
 
 /* Uniform in (0,1): (k + 1/2) * 2^-23 with k the top 23 bits; exactly representable. */

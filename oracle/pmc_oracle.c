@@ -177,8 +177,9 @@ static void subsweep_cell(const pmc_params* p, float* disk, const int16_t* n, in
     int perm[64];
     for (int s = 0; s < n_own; ++s) perm[s] = s;
     for (int i = n_own - 1; i > 0; --i) {
-        pmc_u32x4 w = pmc_philox4x32_10((uint32_t)i, id, sweep, PMC_TAG_SHUFFLE, k0, k1);
-        int j = (int)pmc_bounded(w.v[0], (uint32_t)(i + 1));
+        /* slot i's word: word i & 3 of SHUFFLE call i >> 2 (RNG spec v8, include/pmc_detmath.h) */
+        pmc_u32x4 w = pmc_philox4x32_10((uint32_t)(i >> 2), id, sweep, PMC_TAG_SHUFFLE, k0, k1);
+        int j = (int)pmc_bounded(w.v[i & 3], (uint32_t)(i + 1));
         int t = perm[i]; perm[i] = perm[j]; perm[j] = t;
     }
 

@@ -203,13 +203,166 @@ __device__ __forceinline__ int64_t sidx(const DevGeom& g, int x, int y, int zl) 
 // MIRROR (slab boundary planes): the written-back rows also go to `mirror` -- mirror_mode 0: the
 // packed colour buffer of the halo exchange (row ta + tb*cps_x/2), 1: a plane (row x + cps_x*y;
 // the periodic single-rank halo).  Empty cells write nothing (their count stays 0).
-template <int NSLOT, int NMC, int LCAP, bool OFF32, bool MIRROR = false>
-__device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restrict__ disk,
-                                              const int16_t* __restrict__ ncnt, int ox, int oy, int oz,
-                                              uint32_t sweep, unsigned long long* __restrict__ stats,
-                                              float* __restrict__ px_, int lcap_rt, int cap, int t,
-                                              int cz0, float* __restrict__ mirror = nullptr,
-                                              int mirror_mode = 0) {
+#ifndef PMC_CELLS_PER_WAVE
+#define PMC_CELLS_PER_WAVE 2   // main launch: cells visited per wave (1: the single-cell prologue)
+#endif
+
+// Overflow queue header (ints): [kOvfCount] queued cells, [kOvfDone] fallback workgroups done;
+// entries from kOvfHead.  Zero between launches (the fallback's last workgroup resets it).
+constexpr int kOvfCount = 0, kOvfDone = 1;
+
+// Wave-uniform geometry of one cell visit: t -> (ta, tb, tc) by host-computed magic division
+// (SALU only), the cell's storage index, its global id (the RNG counter) and whether its stencil
+// crosses a box face.
+struct CellGeo {
+    int ta, tb, x, y, zl, zg0;
+    uint32_t c, id;
+    bool edge;
+};
+
+__device__ __forceinline__ CellGeo cell_geo(const DevGeom& g, int t, int cz0, int ox, int oy, int oz) {
+    CellGeo cg;
+    const uint32_t q1 = udiv_magic((uint32_t)t, g.div_ncx);
+    const uint32_t q2 = udiv_magic(q1, g.div_ncy);
+    cg.ta = t - (int)q1 * (g.cps_x >> 1);
+    cg.tb = (int)q1 - (int)q2 * (g.cps_y >> 1);
+    const int tc = cz0 + (int)q2;                          // colour plane (z = 2*tc + oz)
+    cg.x = 2 * cg.ta + ox;
+    cg.y = 2 * cg.tb + oy;
+    cg.zl = 2 * tc + oz;
+    cg.zg0 = g.z0 + cg.zl;
+    const int plane = g.cps_x * g.cps_y;
+    cg.c = (uint32_t)(cg.x + g.cps_x * cg.y + plane * (cg.zl + g.halo));
+    cg.id = (uint32_t)cg.x + (uint32_t)g.cps_x * ((uint32_t)cg.y + (uint32_t)g.cps_y * (uint32_t)cg.zg0);
+    cg.edge = cg.x == 0 || cg.x == g.cps_x - 1 || cg.y == 0 || cg.y == g.cps_y - 1 || cg.zg0 == 0 ||
+              cg.zg0 == g.cps_z - 1;
+    return cg;
+}
+
+// Stencil table of the cell on lanes hb + k, k < 27 (own cell first, then get_neighbors order,
+// subsweep.h:119-137; lane k = 9*hx + 3*hy + hz, h = 0, 1, 2 -> offset 0, -1, +1): storage cell and
+// periodic image (apply_PBC, subsweep.h:139-151).  `edge` is wave-uniform over both halves (the
+// wrapped arithmetic is exact for interior cells too).
+struct StencilLane {
+    uint32_t kc;
+    float sx, sy, sz;
+};
+
+__device__ __forceinline__ StencilLane stencil_lane(const DevGeom& g, const CellGeo& cg, int k, bool edge) {
+    const int dx = (int)bit_of(kStencilPos[0], k) - (int)bit_of(kStencilNeg[0], k);
+    const int dy = (int)bit_of(kStencilPos[1], k) - (int)bit_of(kStencilNeg[1], k);
+    const int dz = (int)bit_of(kStencilPos[2], k) - (int)bit_of(kStencilNeg[2], k);
+    const int plane = g.cps_x * g.cps_y;
+    StencilLane sl;
+    sl.sx = sl.sy = sl.sz = 0.0f;
+    if (!edge) {
+        sl.kc = cg.c + (uint32_t)(dx + g.cps_x * dy + plane * dz);   // (storage is contiguous across halos)
+    } else {
+        // periodic wrap as selects (no exec-mask branches)
+        const int nx0 = cg.x + dx, ny0 = cg.y + dy, zgn = cg.zg0 + dz;
+        const int nx = nx0 + (nx0 < 0 ? g.cps_x : 0) - (nx0 >= g.cps_x ? g.cps_x : 0);
+        const int ny = ny0 + (ny0 < 0 ? g.cps_y : 0) - (ny0 >= g.cps_y ? g.cps_y : 0);
+        sl.sx = nx0 < 0 ? -g.Lx : (nx0 >= g.cps_x ? g.Lx : 0.0f);
+        sl.sy = ny0 < 0 ? -g.Ly : (ny0 >= g.cps_y ? g.Ly : 0.0f);
+        sl.sz = zgn < 0 ? -g.Lz : (zgn >= g.cps_z ? g.Lz : 0.0f);
+        const int nz0 = cg.zl + dz;
+        const int nzl = g.halo ? nz0 : nz0 + (nz0 < 0 ? g.cps_z : 0) - (nz0 >= g.cps_z ? g.cps_z : 0);
+        sl.kc = (uint32_t)(nx + g.cps_x * ny + plane * (nzl + g.halo));
+    }
+    return sl;
+}
+
+// The visit's single HBM round trip: lanes load half rows (slots [0, HS)) of the 26 neighbours
+// (NP passes, CPP cells per pass; row offsets from the stencil lanes hb + k) and the own rows.
+template <int NSLOT, int NMC, bool OFF32>
+struct VisitLoads {
+    static constexpr int HS = stage_split(NSLOT);
+    static constexpr int CPP = kWave / HS;
+    static constexpr int NP = (26 + CPP - 1) / CPP;
+    float vx[NP], vy[NP], vz[NP];
+    float ownx, owny, ownz;
+    __device__ __forceinline__ void issue(const DevGeom& g, const float* __restrict__ disk, const CellGeo& cg,
+                                          uint32_t k_off, int hb) {
+        const int lane = threadIdx.x & (kWave - 1);
+        const int nm = NMC > 0 ? NMC : g.nmax;
+        const int p = lane & (HS - 1);
+        const int kk = lane / HS;
+        const int pp = p < nm ? p : 0;
+        const uint32_t pp_off = (uint32_t)pp * DiskAddr<OFF32>::kUnit;
+        const uint32_t nm_off = (uint32_t)nm * DiskAddr<OFF32>::kUnit;
+#pragma unroll
+        for (int q = 0; q < NP; ++q) {
+            const int k = 1 + q * CPP + kk;
+            const uint32_t off = (uint32_t)__shfl((int)k_off, hb + (k < 27 ? k : 26)) + pp_off;
+            vx[q] = DiskAddr<OFF32>::ld(disk, off);
+            vy[q] = DiskAddr<OFF32>::ld(disk, off + nm_off);
+            vz[q] = DiskAddr<OFF32>::ld(disk, off + 2 * nm_off);
+        }
+        const float* own = disk + (uint64_t)cg.c * (uint32_t)(3 * nm);   // wave-uniform base
+        const int l = lane < nm ? lane : 0;
+        ownx = own[l];
+        owny = own[nm + l];
+        ownz = own[2 * nm + l];
+    }
+};
+
+// Random numbers (RNG spec, include/pmc_detmath.h tags): move m -> Philox(m, id, sweep, MOVE):
+// (w0, w1) Box-Muller pair A -> d0 = s R cos, d1 = s R sin; (w2, w3) pair B -> d2 = s R cos;
+// acceptance threshold of move m -> -log u(Philox(m, id, sweep, ACCEPT).w0); Fisher-Yates word of
+// slot i -> Philox(i >> 2, id, sweep, SHUFFLE).w[i & 3].  Every (cell, move, slot) has its own
+// counter, so the lane mapping below is free: one cell per wave (16 moves per chunk) or two cells per
+// wave (10 moves each in the first chunk) give the same numbers.
+//
+// Parking: move j of the current chunk keeps (d0, d1) at y-row tail pair j and (d2, T) at z-row
+// tail pair j (slots [lcap4, lcap4 + 32): never staged, read by the moves only as "far" partners'
+// don't-care values), so a move takes its randoms with two broadcast LDS reads.
+
+// Single-cell RNG chunk: moves m0..m0+15 -- lanes 0-15 MOVE call (pair A), 16-31 ACCEPT call,
+// 32-47 the MOVE call again (pair B from its words 2, 3: no cross-lane traffic) -- parked.
+__device__ __forceinline__ void rng_chunk_single(const DevGeom& g, uint32_t id, uint32_t sweep, int m0,
+                                                 float* py_, float* pz_, int lcap4) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int j = lane & 15;
+    const uint32_t tag = (lane & 48) == 16 ? PMC_TAG_ACCEPT : PMC_TAG_MOVE;
+    const pmc_u32x4 w = philox_sched((uint32_t)(m0 + j), id, sweep, tag, g);
+    const uint32_t wl = lane < 32 ? w.v[0] : w.v[2];
+    const uint32_t ws = lane < 32 ? w.v[1] : w.v[3];
+    const float lg = pmc_logf(pmc_u01(wl));
+    const float R = __builtin_sqrtf(-2.0f * lg);
+    float sn, cs;
+    pmc_det_sincos_2pi(pmc_u01(ws), &sn, &cs);
+    const float G0 = (R * cs) * g.sigma;   // lanes 0-15: d0 of move m0+j; 32-47: d2
+    const float G1 = (R * sn) * g.sigma;   // lanes 0-15: d1
+    const float TT = -lg;                  // lanes 16-31: T
+    if (lane < 16) *(float2*)(py_ + lcap4 + 2 * j) = make_float2(G0, G1);
+    else if (lane < 48) pz_[lcap4 + 2 * j + (lane < 32 ? 1 : 0)] = lane < 32 ? TT : G0;
+}
+
+// Fisher-Yates indices of slots 0-63 (lane i: slot i): SHUFFLE calls 0-15 on lanes 0-15, their
+// 4 words through LDS scratch `tmp` (64 floats; the term list area, free outside the moves).
+__device__ __forceinline__ int fy_words_single(const DevGeom& g, uint32_t id, uint32_t sweep, float* tmp) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const pmc_u32x4 w = philox_sched((uint32_t)(lane & 15), id, sweep, PMC_TAG_SHUFFLE, g);
+    if (lane < 16) *(uint4*)(tmp + 4 * lane) = make_uint4(w.v[0], w.v[1], w.v[2], w.v[3]);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const uint32_t wi = *(const uint32_t*)(tmp + lane);
+    return (int)pmc_bounded(wi, (uint32_t)(lane + 1));
+}
+
+// One cell visit after its prologue (stencil table + loads issued on lanes hb.., FY words jv on
+// lanes hb + i, first_len moves parked): shuffle, staging, moves, write-back.
+// Returns false (and leaves the cell untouched) when the cell's staged partners do not fit the
+// LDS capacity `cap`; the caller queues it for the full-capacity fallback launch.
+// MIRROR (slab boundary planes): the written-back rows also go to `mirror` -- mirror_mode 0: the
+// packed colour buffer of the halo exchange (row ta + tb*cps_x/2), 1: a plane (row x + cps_x*y;
+// the periodic single-rank halo).  Empty cells write nothing (their count stays 0).
+template <int NSLOT, int NMC, int LCAP, bool OFF32, bool MIRROR>
+__device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__ disk, uint32_t sweep,
+                                           unsigned long long* __restrict__ stats, float* __restrict__ px_,
+                                           int lcap_rt, int cap, int t, const CellGeo& cg, int hb, int k_cnt,
+                                           uint32_t k_off, float k_sx, float k_sy, float k_sz,
+                                           const VisitLoads<NSLOT, NMC, OFF32>& ld, int jv, int fy_have,
+                                           int first_len, float* __restrict__ mirror, int mirror_mode) {
     constexpr int HS = stage_split(NSLOT);        // staging lanes per stencil cell (main passes)
     constexpr int CPP = kWave / HS;               // stencil cells staged per pass
     constexpr int NP = (26 + CPP - 1) / CPP;      // main staging passes over the 26 neighbours
@@ -221,116 +374,27 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     float* py_ = px_ + stride;
     float* pz_ = py_ + stride;
     float* buf = pz_ + stride;                  // term list: signed r2 values
-    // t -> (ta, tb, tc) by host-computed magic division (SALU only)
-    const uint32_t q1 = udiv_magic((uint32_t)t, g.div_ncx);
-    const uint32_t q2 = udiv_magic(q1, g.div_ncy);
-    const int ta = t - (int)q1 * (g.cps_x >> 1);
-    const int tb = (int)q1 - (int)q2 * (g.cps_y >> 1);
-    const int tc = cz0 + (int)q2;                          // colour plane (z = 2*tc + oz)
-    const int x = 2 * ta + ox, y = 2 * tb + oy, zl = 2 * tc + oz;
-    const int zg0 = g.z0 + zl;
-    const int plane = g.cps_x * g.cps_y;
-    const uint32_t c = (uint32_t)(x + g.cps_x * y + plane * (zl + g.halo));
-    const uint32_t id = (uint32_t)x + (uint32_t)g.cps_x * ((uint32_t)y + (uint32_t)g.cps_y * (uint32_t)zg0);
-    const uint32_t row = (uint32_t)(3 * nm);                 // floats per cell
-
-    PMC_STAMP(0);
-    // ---- 1. stencil table (lane k < 27; lanes >= 27 compute some in-range cell, unused) -------
-    // lane k = 9*hx + 3*hy + hz, h = 0, 1, 2 -> offset 0, -1, +1 (get_neighbors order)
-    const int dx = (int)bit_of(kStencilPos[0], lane) - (int)bit_of(kStencilNeg[0], lane);
-    const int dy = (int)bit_of(kStencilPos[1], lane) - (int)bit_of(kStencilNeg[1], lane);
-    const int dz = (int)bit_of(kStencilPos[2], lane) - (int)bit_of(kStencilNeg[2], lane);
-    // periodic images only matter for cells on the box faces (apply_PBC, subsweep.h:139-151):
-    // interior waves (~95% at 128^3) take the plain offsets, face waves the wrapped ones
-    const bool edge = x == 0 || x == g.cps_x - 1 || y == 0 || y == g.cps_y - 1 || zg0 == 0 ||
-                      zg0 == g.cps_z - 1;
-    uint32_t kc;
-    float k_sx = 0.0f, k_sy = 0.0f, k_sz = 0.0f;
-    if (!edge) {
-        kc = c + (uint32_t)(dx + g.cps_x * dy + plane * dz);   // (storage is contiguous across halos)
-    } else {
-        // periodic wrap as selects (no exec-mask branches)
-        const int nx0 = x + dx, ny0 = y + dy, zgn = zg0 + dz;
-        const int nx = nx0 + (nx0 < 0 ? g.cps_x : 0) - (nx0 >= g.cps_x ? g.cps_x : 0);
-        const int ny = ny0 + (ny0 < 0 ? g.cps_y : 0) - (ny0 >= g.cps_y ? g.cps_y : 0);
-        k_sx = nx0 < 0 ? -g.Lx : (nx0 >= g.cps_x ? g.Lx : 0.0f);
-        k_sy = ny0 < 0 ? -g.Ly : (ny0 >= g.cps_y ? g.Ly : 0.0f);
-        k_sz = zgn < 0 ? -g.Lz : (zgn >= g.cps_z ? g.Lz : 0.0f);
-        const int nz0 = zl + dz;
-        const int nzl = g.halo ? nz0 : nz0 + (nz0 < 0 ? g.cps_z : 0) - (nz0 >= g.cps_z ? g.cps_z : 0);
-        kc = (uint32_t)(nx + g.cps_x * ny + plane * (nzl + g.halo));
-    }
-    const int k_cnt = ncnt[kc];
-    const uint32_t k_off = kc * row * DiskAddr<OFF32>::kUnit;   // bytes (OFF32) or floats
+    const int ta = cg.ta, tb = cg.tb, x = cg.x, y = cg.y, zg0 = cg.zg0;
+    const uint32_t c = cg.c, id = cg.id;
+    const bool edge = cg.edge;
     const int p = lane & (HS - 1);
     const int kk = lane / HS;
-    const int pp = p < nm ? p : 0;
-    const uint32_t pp_off = (uint32_t)pp * DiskAddr<OFF32>::kUnit;
     const uint32_t nm_off = (uint32_t)nm * DiskAddr<OFF32>::kUnit;
-    PMC_STAMP(1);
-    float vx[NP], vy[NP], vz[NP];
-#pragma unroll
-    for (int q = 0; q < NP; ++q) {
-        const int k = 1 + q * CPP + kk;
-        const uint32_t off = (uint32_t)__shfl((int)k_off, k < 27 ? k : 26) + pp_off;
-        vx[q] = DiskAddr<OFF32>::ld(disk, off);
-        vy[q] = DiskAddr<OFF32>::ld(disk, off + nm_off);
-        vz[q] = DiskAddr<OFF32>::ld(disk, off + 2 * nm_off);
-    }
-    float ownx, owny, ownz;
-    {
-        const float* own = disk + (uint64_t)c * row;           // wave-uniform base
-        const int l = lane < nm ? lane : 0;
-        ownx = own[l];
-        owny = own[nm + l];
-        ownz = own[2 * nm + l];
-    }
-
-    PMC_STAMP(2);
-    // ---- 2. random numbers for the first 16 moves + the shuffle (overlaps the loads) ------------
-    float G0 = 0.0f, G1 = 0.0f, TT = 0.0f;
-    int jv = 0;
-    auto rng_chunk = [&](int m0, bool first) {
-        uint32_t idx, tag;
-        if (lane < 16) { idx = (uint32_t)(m0 + lane); tag = PMC_TAG_MOVE; }
-        else if (lane < 32) { idx = (uint32_t)(m0 + lane - 16); tag = PMC_TAG_ACCEPT; }
-        else { idx = (uint32_t)(lane - 32); tag = PMC_TAG_SHUFFLE; }
-        const pmc_u32x4 w = philox_sched(idx, id, sweep, tag, g);
-        if (first) {
-            const int jraw = (int)pmc_bounded(w.v[0], (uint32_t)(lane - 32 + 1));
-            jv = __shfl(jraw, (lane + 32) & 63);                  // slot i's FY index in lane i
-        }
-        const uint32_t b2 = (uint32_t)__shfl((int)w.v[2], lane & 15);
-        const uint32_t b3 = (uint32_t)__shfl((int)w.v[3], lane & 15);
-        const uint32_t wl = lane < 32 ? w.v[0] : b2;
-        const uint32_t ws = lane < 32 ? w.v[1] : b3;
-        const float lg = pmc_logf(pmc_u01(wl));
-        const float R = __builtin_sqrtf(-2.0f * lg);
-        float sn, cs;
-        pmc_det_sincos_2pi(pmc_u01(ws), &sn, &cs);
-        G0 = (R * cs) * g.sigma;   // lanes 0-15: g0*sigma of move m0+lane; 32-47: g2*sigma
-        G1 = (R * sn) * g.sigma;   // lanes 0-15: g1*sigma
-        TT = -lg;         // lanes 16-31: acceptance threshold of move m0+lane-16
-        // park move j's randoms in the unused tails of the y / z rows (slots [lcap4, lcap4 + 32):
-        // never staged, read by the moves only as "far" partners' don't-care values): (d0, d1) at
-        // y-tail pair j, (d2, T) at z-tail pair j.  A move then takes them with two broadcast LDS
-        // reads off one address instead of four v_readlane.
-        {
-            const int j = lane & 15;
-            if (lane < 16) *(float2*)(py_ + lcap4 + 2 * j) = make_float2(G0, G1);
-            else if (lane < 48) pz_[lcap4 + 2 * j + (lane < 32 ? 1 : 0)] = lane < 32 ? TT : G0;
-        }
-    };
-    rng_chunk(0, true);
-    PMC_STAMP(3);
-
-    const int n_own = __builtin_amdgcn_readfirstlane(k_cnt);   // lane 0 = own cell
+    const float (&vx)[NP] = ld.vx;
+    const float (&vy)[NP] = ld.vy;
+    const float (&vz)[NP] = ld.vz;
+    const float ownx = ld.ownx, owny = ld.owny, ownz = ld.ownz;
+    // single-cell RNG chunk: moves m0..m0+15 (lanes 0-15 MOVE, 16-31 ACCEPT, 32-47 pair B), parked
+    auto rng_single = [&](int m0) { rng_chunk_single(g, id, sweep, m0, py_, pz_, lcap4); };
+    const int n_own = __builtin_amdgcn_readlane(k_cnt, hb);    // lane hb = own cell
     if (n_own == 0) return true;                                // subsweep.h:252-253
     PMC_STAMP(4);
     const int cap_nb = cap - n_own;
-    if (n_own > 32) {     // nmax > 32: Fisher-Yates words of slots 32..63
-        const pmc_u32x4 w = philox_sched((uint32_t)lane, id, sweep, PMC_TAG_SHUFFLE, g);
-        if (lane >= 32) jv = (int)pmc_bounded(w.v[0], (uint32_t)(lane + 1));
+    // slot i's Fisher-Yates index sits on lane jb + i (the prologue's layout: the cell's half)
+    int jb = hb;
+    if (n_own > fy_have) {                         // rare: slots beyond the prologue's, on lane i
+        jv = fy_words_single(g, id, sweep, buf);
+        jb = 0;
     }
 
     // ---- Fisher-Yates shuffle of the own cell (random_shuffle, subsweep.h:50-58; fixes R1) ---
@@ -340,7 +404,7 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
         // SGPRs (no VGPR read-modify-write chain through v_readlane), one VALU unpack at the end
         uint64_t P = 0xFEDCBA9876543210ull;
         for (int i = n_own - 1; i > 0; --i) {
-            const uint32_t j = (uint32_t)__builtin_amdgcn_readlane(jv, i);
+            const uint32_t j = (uint32_t)__builtin_amdgcn_readlane(jv, jb + i);
             const uint32_t si = 4u * (uint32_t)i, sj = 4u * j;
             const uint64_t d = ((P >> si) ^ (P >> sj)) & 15u;   // a[i] ^ a[j]
             P ^= (d << si) | (d << sj);                        // swap (d == 0 when i == j)
@@ -349,7 +413,7 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     } else {
         perm = lane;
         for (int i = n_own - 1; i > 0; --i) {
-            const int j = __builtin_amdgcn_readlane(jv, i);
+            const int j = __builtin_amdgcn_readlane(jv, jb + i);
             const int vi = __builtin_amdgcn_readlane(perm, i);
             const int vj = __builtin_amdgcn_readlane(perm, j);
             perm = lane == i ? vj : (lane == j ? vi : perm);
@@ -381,12 +445,12 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
         for (int q = 0; q < NP; ++q) {
             const int k = 1 + q * CPP + kk;
             const int ks = k < 27 ? k : 26;
-            const int cnt = __shfl(k_cnt, ks);
+            const int cnt = __shfl(k_cnt, hb + ks);
             float ux = vx[q], uy = vy[q], uz = vz[q];
             if constexpr (decltype(with_image)::value) {
-                ux = ux + __shfl(k_sx, ks);
-                uy = uy + __shfl(k_sy, ks);
-                uz = uz + __shfl(k_sz, ks);
+                ux = ux + __shfl(k_sx, hb + ks);
+                uy = uy + __shfl(k_sy, hb + ks);
+                uz = uz + __shfl(k_sz, hb + ks);
             }
             // lanes of stencil cells k < 27 (compile-time per pass), slot < count, box filter
             const unsigned long long live = stage_lane_mask<HS>(q);
@@ -396,9 +460,9 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
             // overflow passes: slots [HS, nmax) of the neighbours holding more than HS particles,
             // in stencil order, CPP cells per pass (lane group j: the j-th remaining cell); loads
             // issued here (the rare case pays its own round trip)
-            unsigned long long ovm = __builtin_amdgcn_ballot_w64(lane >= 1 && lane < 27 && k_cnt > HS);
+            unsigned long long ovm = __builtin_amdgcn_ballot_w64(lane >= hb + 1 && lane < hb + 27 && k_cnt > HS);
             while (ovm) {
-                int ks = 26, ncell = 0;
+                int ks = hb + 26, ncell = 0;
                 for (; ncell < CPP && ovm; ++ncell) {
                     const int kb = (int)__builtin_ctzll(ovm);
                     ovm &= ovm - 1ull;
@@ -464,9 +528,10 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     // block code with no per-move loop or bound tests (the full-capacity launches keep the loop).
     auto move_loop = [&](auto nb_c) {
     constexpr int NB = decltype(nb_c)::value;
-    for (int m0 = 0; m0 < g.n_moves; m0 += 16) {
-        if (m0 > 0) rng_chunk(m0, false);
-        const int mend = wave_uniform((g.n_moves - m0) < 16 ? (g.n_moves - m0) : 16);
+    for (int m0 = 0; m0 < g.n_moves; m0 += (m0 == 0 ? first_len : 16)) {
+        if (m0 > 0) rng_single(m0);
+        const int clen = m0 == 0 ? first_len : 16;
+        const int mend = wave_uniform((g.n_moves - m0) < clen ? (g.n_moves - m0) : clen);
         const float* mvp = py_ + lcap4;                    // this chunk's move randoms (y tail)
         for (int ml = 0; ml < mend; ++ml, mvp += 2) {
             const float2 mva = *(const float2*)mvp;            // (d0, d1)
@@ -597,15 +662,135 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     return true;
 }
 
-// Overflow queue header (ints): [kOvfCount] queued cells, [kOvfDone] fallback workgroups done;
-// entries from kOvfHead.  Zero between launches (the fallback's last workgroup resets it).
-constexpr int kOvfCount = 0, kOvfDone = 1;
+// The single-cell prologue: stencil table on lanes 0-26, the visit's loads, then one RNG pass
+// (moves 0-15 and FY words of slots 0-63) while the loads fly.
+template <int NSLOT, int NMC, int LCAP, bool OFF32, bool MIRROR = false>
+__device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restrict__ disk,
+                                              const int16_t* __restrict__ ncnt, int ox, int oy, int oz,
+                                              uint32_t sweep, unsigned long long* __restrict__ stats,
+                                              float* __restrict__ px_, int lcap_rt, int cap, int t,
+                                              int cz0, float* __restrict__ mirror = nullptr,
+                                              int mirror_mode = 0) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int nm = NMC > 0 ? NMC : g.nmax;
+    const int lcap = LCAP > 0 ? LCAP : lcap_rt;
+    const int stride = subsweep_stride(lcap);
+    const int lcap4 = (lcap + 3) & ~3;
+    float* py_ = px_ + stride;
+    float* pz_ = py_ + stride;
+    float* buf = pz_ + stride;
+    const CellGeo cg = cell_geo(g, t, cz0, ox, oy, oz);
+    PMC_STAMP(0);
+    const StencilLane sl = stencil_lane(g, cg, lane, cg.edge);
+    const int k_cnt = ncnt[sl.kc];
+    const uint32_t k_off = sl.kc * (uint32_t)(3 * nm) * DiskAddr<OFF32>::kUnit;   // bytes (OFF32) or floats
+    PMC_STAMP(1);
+    VisitLoads<NSLOT, NMC, OFF32> ld;
+    ld.issue(g, disk, cg, k_off, 0);
+    PMC_STAMP(2);
+    rng_chunk_single(g, cg.id, sweep, 0, py_, pz_, lcap4);
+    const int jv = fy_words_single(g, cg.id, sweep, buf);
+    PMC_STAMP(3);
+    return visit_cell<NSLOT, NMC, LCAP, OFF32, MIRROR>(g, disk, sweep, stats, px_, lcap_rt, cap, t, cg, 0, k_cnt,
+                                                       k_off, sl.sx, sl.sy, sl.sz, ld, jv, 64, 16, mirror,
+                                                       mirror_mode);
+}
+
+// The two-cell prologue (main launch): cells tA (lanes 0-31) and tB (lanes 32-63) of one colour,
+// never neighbours.  One stencil table for both (cell A's on lanes 0-26, B's on 32-58), one Philox
+// pass and one log/sqrt/sincos pass for both cells' first 10 moves and Fisher-Yates slots 0-15:
+//   Philox lane h + l:  l < 10 MOVE call l, 10 <= l < 20 ACCEPT call l-10, 20 <= l < 24 SHUFFLE call l-20
+//   transform lane h + l:  l < 10 pair A of move l, 10 <= l < 20 pair B of move l-10,
+//                          20 <= l < 30 -log u of move l-20
+// (h = 0 for A, 32 for B).  Cell A is visited with its rows loaded up front; B's randoms wait in
+// registers and its loads go out after A.
+template <int NSLOT, int NMC, bool OFF32>
+__device__ __forceinline__ void subsweep_pair(const DevGeom& g, float* __restrict__ disk,
+                                              const int16_t* __restrict__ ncnt, int ox, int oy, int oz,
+                                              uint32_t sweep, unsigned long long* __restrict__ stats,
+                                              float* __restrict__ px_, int cap, int tA, bool hasB, int cz0,
+                                              int* __restrict__ ovf) {
+    constexpr int LCAP = kMainCap;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int nm = NMC > 0 ? NMC : g.nmax;
+    constexpr int stride = subsweep_stride(LCAP);
+    constexpr int lcap4 = (LCAP + 3) & ~3;
+    float* py_ = px_ + stride;
+    float* pz_ = py_ + stride;
+    float* buf = pz_ + stride;
+    const int h = lane & 32;                       // 0: cell A's half, 32: cell B's
+    const int l = lane & 31;
+    const CellGeo ca = cell_geo(g, tA, cz0, ox, oy, oz);
+    const CellGeo cb = cell_geo(g, hasB ? tA + 1 : tA, cz0, ox, oy, oz);
+    // ---- stencil tables of both cells, counts ----------------------------------------------
+    CellGeo cl = ca;                               // this lane's cell (per-lane selects)
+    cl.x = h ? cb.x : ca.x;
+    cl.y = h ? cb.y : ca.y;
+    cl.zl = h ? cb.zl : ca.zl;
+    cl.zg0 = h ? cb.zg0 : ca.zg0;
+    cl.c = h ? cb.c : ca.c;
+    const StencilLane sl = stencil_lane(g, cl, l, ca.edge || cb.edge);
+    const int k_cnt = ncnt[sl.kc];
+    const uint32_t k_off = sl.kc * (uint32_t)(3 * nm) * DiskAddr<OFF32>::kUnit;
+    VisitLoads<NSLOT, NMC, OFF32> ld;
+    ld.issue(g, disk, ca, k_off, 0);
+    // ---- one RNG pass for both cells ---------------------------------------------------------
+    const uint32_t idl = h ? cb.id : ca.id;
+    uint32_t idx, tag;
+    if (l < 10) { idx = (uint32_t)l; tag = PMC_TAG_MOVE; }
+    else if (l < 20) { idx = (uint32_t)(l - 10); tag = PMC_TAG_ACCEPT; }
+    else { idx = (uint32_t)(l - 20); tag = PMC_TAG_SHUFFLE; }
+    const pmc_u32x4 w = philox_sched(idx, idl, sweep, tag, g);
+    // Fisher-Yates words of slots 0-15 of both cells through LDS (the term list area is free):
+    // SHUFFLE call k's 4 words are slots 4k..4k+3; lane h + i takes slot i's
+    if (l >= 20 && l < 24) *(uint4*)(buf + (h >> 1) + 4 * (l - 20)) = make_uint4(w.v[0], w.v[1], w.v[2], w.v[3]);
+    // transform inputs: lanes l < 10 their own (w0, w1); 10-19 (w2, w3) of MOVE lane l-10;
+    // 20-29 w0 of ACCEPT lane l-10
+    const int src = h + (l < 10 ? l : l - 10);
+    const uint32_t s0 = (uint32_t)__shfl((int)w.v[0], src);
+    const uint32_t s2 = (uint32_t)__shfl((int)w.v[2], src);
+    const uint32_t s3 = (uint32_t)__shfl((int)w.v[3], src);
+    const uint32_t wl = l < 10 ? w.v[0] : (l < 20 ? s2 : s0);
+    const uint32_t ws = l < 10 ? w.v[1] : s3;
+    const float lg = pmc_logf(pmc_u01(wl));
+    const float R = __builtin_sqrtf(-2.0f * lg);
+    float sn, cs;
+    pmc_det_sincos_2pi(pmc_u01(ws), &sn, &cs);
+    const float G0 = (R * cs) * g.sigma;          // l < 10: d0; 10-19: d2
+    const float G1 = (R * sn) * g.sigma;          // l < 10: d1
+    const float TT = -lg;                         // 20-29: T
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const int fyw = (int)*(const uint32_t*)(buf + (h >> 1) + (l & 15));
+    const int jv = (int)pmc_bounded((uint32_t)fyw, (uint32_t)((l & 15) + 1));
+    // park cell h's first 10 moves (h = 0 now, 32 before B's visit)
+    auto park = [&](int hh) {
+        const int j = l < 10 ? l : (l < 20 ? l - 10 : l - 20);
+        if ((lane & 32) == hh && l < 30) {
+            if (l < 10) *(float2*)(py_ + lcap4 + 2 * j) = make_float2(G0, G1);
+            else pz_[lcap4 + 2 * j + (l < 20 ? 0 : 1)] = l < 20 ? G0 : TT;
+        }
+    };
+    park(0);
+    if (!visit_cell<NSLOT, NMC, LCAP, OFF32, false>(g, disk, sweep, stats, px_, LCAP, cap, tA, ca, 0, k_cnt, k_off,
+                                                    sl.sx, sl.sy, sl.sz, ld, jv, 16, 10, nullptr, 0)) {
+        if (lane == 0) ovf[kOvfHead + atomicAdd(&ovf[kOvfCount], 1)] = tA;
+    }
+    if (!hasB) return;
+    park(32);
+    ld.issue(g, disk, cb, k_off, 32);
+    if (!visit_cell<NSLOT, NMC, LCAP, OFF32, false>(g, disk, sweep, stats, px_, LCAP, cap, tA + 1, cb, 32, k_cnt,
+                                                    k_off, sl.sx, sl.sy, sl.sz, ld, jv, 16, 10, nullptr, 0)) {
+        if (lane == 0) ovf[kOvfHead + atomicAdd(&ovf[kOvfCount], 1)] = tA + 1;
+    }
+}
+
 
 // Main launch: one wave per cell of the colour; LDS layout for kMainCap partners, capacity `cap`
 // (<= kMainCap) partners per wave (sized for the occupancy; a cell whose filtered stencil
 // exceeds it is queued in ovf for the fallback).
+// amdgpu_waves_per_eu(8): 8 waves per SIMD (what the 5 KiB LDS slots allow) also bounds the SGPRs
 template <int NSLOT, int NMC, bool OFF32>
-__global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep(DevGeom g, float* __restrict__ disk,
+__global__ __launch_bounds__(kWave * kSubWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_subsweep(DevGeom g, float* __restrict__ disk,
                                                                   const int16_t* __restrict__ ncnt,
                                                                   int ox, int oy, int oz, uint32_t sweep,
                                                                   unsigned long long* __restrict__ stats,
@@ -618,12 +803,19 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep(DevGeom g, float
     uint32_t nblk = gridDim.x, b = blockIdx.x;
     if ((nblk & 7u) == 0u) b = (b & 7u) * (nblk >> 3) + (b >> 3);
     const int total = (g.cps_x >> 1) * (g.cps_y >> 1) * ncz;
+#if PMC_CELLS_PER_WAVE == 2
+    // two cells per wave (shared stencil table and RNG pass): wave w takes cells 2w and 2w+1
+    const int t = 2 * ((int)b * kSubWaves + wv);
+    if (t >= total) return;
+    subsweep_pair<NSLOT, NMC, OFF32>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, cap, t, t + 1 < total, cz0, ovf);
+#else
     const int t = (int)b * kSubWaves + wv;
     if (t >= total) return;
     if (!subsweep_wave<NSLOT, NMC, kMainCap, OFF32>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, kMainCap, cap,
                                                 t, cz0)) {
         if ((threadIdx.x & (kWave - 1)) == 0) ovf[kOvfHead + atomicAdd(&ovf[kOvfCount], 1)] = t;
     }
+#endif
 }
 
 // Boundary-plane launch of the slab driver: full capacity (27*nmax partners per wave: no overflow
@@ -977,7 +1169,8 @@ static void launch_subsweep_t(const DevGeom& g, float* disk, const int16_t* n, i
                               uint32_t sweep, unsigned long long* stats, int* ovf, int cz0, int ncz,
                               hipStream_t st) {
     const int64_t total = (int64_t)(g.cps_x / 2) * (g.cps_y / 2) * ncz;
-    const int64_t blocks = (total + kSubWaves - 1) / kSubWaves;
+    const int64_t waves = (total + PMC_CELLS_PER_WAVE - 1) / PMC_CELLS_PER_WAVE;
+    const int64_t blocks = (waves + kSubWaves - 1) / kSubWaves;
     const int cap = subsweep_capacity(g);
     const int full = 27 * g.nmax;
     const size_t lds = sizeof(float) * (size_t)lds_floats_per_wave(kMainCap) * kSubWaves;

@@ -138,6 +138,40 @@ def test_full_sweeps_parity_16(pmc, oracle):
     assert abs(r["e_initial"] + r["de_fixed"] / 2**32 - r["e_final"]) < 1e-3 * abs(r["e_final"])
 
 
+@pytest.mark.parametrize("n_moves", [0, 1, 7, 11, 23, 42])
+def test_move_count_chunking_parity(pmc, oracle, n_moves):
+    """Move counts across the RNG chunk boundaries (the two-cell prologue parks 10 moves per cell,
+    further chunks hold 16; the single-cell path 16 per chunk) give the oracle's result bit for bit."""
+    ctx = _ctx(pmc, 16, n_moves=n_moves)
+    ctx.init_lattice(10_000)
+    st = _ostate(oracle, 16, n_moves=n_moves)
+    st.init_lattice(10_000)
+    r = ctx.start(0, 2)
+    assert st.run(0, 2) == 0
+    _assert_same(oracle, ctx, st, 16)
+    o = st.stats.as_dict()
+    for k in ("de_fixed", "accepted", "trials", "evaluated"):
+        assert r[k] == o[k], k
+
+
+@pytest.mark.parametrize("cps", [(10, 6, 14), (14, 10, 6)])
+def test_odd_colour_count_parity(pmc, oracle, cps):
+    """Rectangular boxes whose colour phases hold an odd number of cells (the last wave of the
+    two-cell main launch visits one cell) equal the oracle bit for bit."""
+    cx, cy, cz = cps
+    atoms = 3 * cx * cy * cz
+    ctx = _ctx(pmc, cx, cps_y=cy, cps_z=cz)
+    ctx.init_lattice(atoms)
+    st = _ostate(oracle, cx, cps_y=cy, cps_z=cz)
+    st.init_lattice(atoms)
+    r = ctx.start(0, 3)
+    assert st.run(0, 3) == 0
+    _assert_same(oracle, ctx, st, 16)
+    o = st.stats.as_dict()
+    for k in ("de_fixed", "accepted", "trials", "evaluated"):
+        assert r[k] == o[k], k
+
+
 def test_graph_replay_equals_eager(pmc):
     a = _ctx(pmc, 16)
     b = _ctx(pmc, 16)
