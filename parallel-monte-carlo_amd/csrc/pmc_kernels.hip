@@ -902,7 +902,7 @@ __global__ __launch_bounds__(256) void k_shift(DevGeom g, const float* __restric
     const unsigned long long below = (1ull << p) - 1ull;
 
     bool live[U];
-    uint32_t c[U];
+    uint32_t c[U], cnbv[U];
     int ncur[U], nnb[U];
     float offset[U], offset_nb[U], own[U][3], nbv[U][3];
 #pragma unroll
@@ -924,6 +924,8 @@ __global__ __launch_bounds__(256) void k_shift(DevGeom g, const float* __restric
         const int nc0 = nin[c[j]], nn0 = nin[cnb];
         ncur[j] = live[j] ? nc0 : 0;
         nnb[j] = live[j] ? nn0 : 0;
+        cnbv[j] = cnb;
+#ifndef PMC_SHIFT_MASKED
         const uint64_t oc = (uint64_t)c[j] * (uint64_t)(3 * nm) + (uint64_t)pp;
         const uint64_t on = (uint64_t)cnb * (uint64_t)(3 * nm) + (uint64_t)pp;
 #pragma unroll
@@ -931,7 +933,21 @@ __global__ __launch_bounds__(256) void k_shift(DevGeom g, const float* __restric
             own[j][dim] = din[oc + (uint64_t)(dim * nm)];
             nbv[j][dim] = din[on + (uint64_t)(dim * nm)];
         }
+#endif
     }
+#ifdef PMC_SHIFT_MASKED
+    // second round trip: only the occupied slots (partial rows: 32 B requests instead of lines)
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+        const uint64_t oc = (uint64_t)c[j] * (uint64_t)(3 * nm) + (uint64_t)pp;
+        const uint64_t on = (uint64_t)cnbv[j] * (uint64_t)(3 * nm) + (uint64_t)pp;
+#pragma unroll
+        for (int dim = 0; dim < 3; ++dim) {
+            own[j][dim] = p < ncur[j] ? din[oc + (uint64_t)(dim * nm)] : 0.0f;
+            nbv[j][dim] = p < nnb[j] ? din[on + (uint64_t)(dim * nm)] : 0.0f;
+        }
+    }
+#endif
 #pragma unroll
     for (int j = 0; j < U; ++j) {
         const float xf = f == 0 ? own[j][0] : (f == 1 ? own[j][1] : own[j][2]);
@@ -1252,7 +1268,7 @@ hipError_t launch_subsweep(const DevGeom& g, float* disk, const int16_t* n, int 
 hipError_t launch_shift(const DevGeom& g, const float* din, const int16_t* nin, float* dout,
                         int16_t* nout, int f, float d, uint32_t* flags, hipStream_t st) {
 #ifndef PMC_SHIFT_U
-#define PMC_SHIFT_U 4
+#define PMC_SHIFT_U 8
 #endif
     constexpr int U = PMC_SHIFT_U;   // cells per lane group, loads hoisted
     const int cpb = 256 / g.nslot;
