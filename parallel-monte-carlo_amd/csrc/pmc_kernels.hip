@@ -2,7 +2,9 @@
 //
 // Reference semantics: subsweep.h (root, "Version I": thread per cell) for the call surface and
 // move rules; the LDS-staging design of CUDA-Parallel-MC/CUDA-Parallel-MC/kernel.cu:209-435
-// ("Version II": block per cell) re-targeted to ONE 64-lane wavefront per cell:
+// ("Version II": block per cell) re-targeted to ONE 64-lane wavefront per cell visit (the main
+// launch gives a wave two cells of the colour, visited one after the other, sharing their
+// stencil-table and random-number passes):
 //   * the cell's 27-cell stencil (own cell first, shuffled; then the 26 neighbours in
 //     get_neighbors order, subsweep.h:119-137) is staged once into LDS (SoA x/y/z), with the
 //     periodic image (apply_PBC, subsweep.h:139-151) folded into the staged coordinates;
@@ -174,16 +176,16 @@ __device__ __forceinline__ int64_t sidx(const DevGeom& g, int x, int y, int zl) 
 }
 
 // ------------------------------------------------------------------------------------------
-// subsweep: one colour phase, one wave per cell (subsweep_kernel, subsweep.h:240-300)
+// subsweep: one colour phase, one wave per cell visit (subsweep_kernel, subsweep.h:240-300)
 //
-// Per cell visit (one wave):
+// Per cell visit (one wave; two per wave in the main launch, see subsweep_pair):
 //   1. stencil table: lane k < 27 computes stencil cell k's storage offset and periodic image
 //      and loads its count; every global load of the visit is issued at once (counts, the 26
-//      neighbours' full rows -- a 64 B row sits inside one 128 B line, so the unused slots cost
-//      no extra lines -- and the own rows): one HBM round trip per visit;
-//   2. RNG while the loads fly, ONE Philox call per lane: lanes 0-15 trial moves, 16-31
-//      acceptance thresholds, 32-63 Fisher-Yates words; then one log + one sincos per lane
-//      (lanes 0-15 Box-Muller pair A, 32-47 pair B with words swizzled in, 16-31 -log u);
+//      neighbours' half rows -- a 64 B row sits inside one 128 B line -- and the own rows): one
+//      HBM round trip per visit;
+//   2. RNG while the loads fly (Philox counters per cell, move, slot; RNG spec above
+//      rng_chunk_single): Box-Muller moves, -log u thresholds, Fisher-Yates words, the moves'
+//      variates parked in LDS;
 //   3. stage the neighbours into LDS, keeping (ballot + mbcnt compaction) only partners within
 //      the cutoff of the own cell's box -- the others contribute exactly 0 -- then the own cell
 //      (shuffled) after them;
