@@ -530,25 +530,50 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
     // block code with no per-move loop or bound tests (the full-capacity launches keep the loop).
     auto move_loop = [&](auto nb_c) {
     constexpr int NB = decltype(nb_c)::value;
+    unsigned long long pend = 0;                       // in-cell moves of the current round
     for (int m0 = 0; m0 < g.n_moves; m0 += (m0 == 0 ? first_len : 16)) {
         if (m0 > 0) rng_single(m0);
         const int clen = m0 == 0 ? first_len : 16;
         const int mend = wave_uniform((g.n_moves - m0) < clen ? (g.n_moves - m0) : clen);
-        const float* mvp = py_ + lcap4;                    // this chunk's move randoms (y tail)
-        for (int ml = 0; ml < mend; ++ml, mvp += 2) {
-            const float2 mva = *(const float2*)mvp;            // (d0, d1)
-            const float2 mvb = *(const float2*)(mvp + stride); // (d2, T) in the z tail
-            const float d0 = mva.x, d1 = mva.y, d2 = mvb.x, Tm = mvb.y;
-            const int si = S_nb + i;
-            const float xi = px_[si], yi = py_[si], zi = pz_[si];
-            const float qx = xi + d0;                  // make_move: x + g * sigma
-            const float qy = yi + d1;
-            const float qz = zi + d2;
-            const float ddx = qx - cxf, ddy = qy - cyf, ddz = qz - czf;
-            // (d > hw || d < -hw) == (|d| > hw) for non-NaN d; |d| is a free source modifier
-            const bool out = (__builtin_fabsf(ddx) > hw) || (__builtin_fabsf(ddy) > hw) ||
-                             (__builtin_fabsf(ddz) > hw);
-            if (!out) {
+        float* mvs = py_ + lcap4;                          // this chunk's move slots (y / z tails)
+        // Rounds of up to n_own consecutive moves: moves cycle through the shuffled particles
+        // (i = m mod n_own, subsweep.h:284-296), so the moves of a round touch different
+        // particles and each one's trial position depends only on its particle's current
+        // position.  Lane j forms move r0 + j's trial position and its out_of_bound test
+        // (subsweep.h:73-88) in parallel, parks (qx, qy | qz) over the move's (d0, d1 | d2), and
+        // only the in-cell moves run one after the other, in order.  Same arithmetic, same order
+        // of state updates as one move at a time: bit for bit.
+        for (int r0 = 0; r0 < mend;) {
+            const int L = wave_uniform((mend - r0) < n_own ? (mend - r0) : n_own);
+            {
+                const int jl = lane < L ? lane : 0;
+                const int pj = (i + jl) >= n_own ? i + jl - n_own : i + jl;
+                float* slot = mvs + 2 * (r0 + jl);
+                const float2 mva = *(const float2*)slot;            // (d0, d1)
+                const float d2 = slot[stride];                      // d2 (z tail)
+                const int sp = S_nb + pj;
+                const float qx = px_[sp] + mva.x;                   // make_move: x + g * sigma
+                const float qy = py_[sp] + mva.y;
+                const float qz = pz_[sp] + d2;
+                // (d > hw || d < -hw) == (|d| > hw) for non-NaN d; |d| is a free source modifier
+                const bool out = (__builtin_fabsf(qx - cxf) > hw) || (__builtin_fabsf(qy - cyf) > hw) ||
+                                 (__builtin_fabsf(qz - czf) > hw);
+                if (lane < L) {
+                    *(float2*)slot = make_float2(qx, qy);
+                    slot[stride] = qz;
+                }
+                pend = __builtin_amdgcn_ballot_w64(!out) & ((1ull << L) - 1ull);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            }
+            while (pend) {
+                const int j = (int)__builtin_ctzll(pend);
+                pend &= pend - 1ull;
+                const float* slot = mvs + 2 * (r0 + j);
+                const float2 qa = *(const float2*)slot;             // (qx, qy)
+                const float2 qb = *(const float2*)(slot + stride);  // (qz, T)
+                const float qx = qa.x, qy = qa.y, qz = qb.x, Tm = qb.y;
+                const int si = S_nb + ((i + j) >= n_own ? i + j - n_own : i + j);
+                const float xi = px_[si], yi = py_[si], zi = pz_[si];
                 ++n_ev;
                 px_[si] = kFar;          // exclude the moving particle from its own term list
                 // 4a. term list: per block of 64 partners, the new-position terms within the
@@ -619,8 +644,9 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
                     de_cell = de_cell + (double)dEu;
                 }
             }
-            i += 1;
-            if (i >= n_own) i = 0;
+            i += L;
+            if (i >= n_own) i -= n_own;
+            r0 += L;
         }
     }
     };
