@@ -531,6 +531,7 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
     auto move_loop = [&](auto nb_c) {
     constexpr int NB = decltype(nb_c)::value;
     unsigned long long pend = 0;                       // in-cell moves of the current round
+    int sp_l = 0;                                      // lane j: row slot of the round's move j
     for (int m0 = 0; m0 < g.n_moves; m0 += (m0 == 0 ? first_len : 16)) {
         if (m0 > 0) rng_single(m0);
         const int clen = m0 == 0 ? first_len : 16;
@@ -563,6 +564,7 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
                     slot[stride] = qz;
                 }
                 pend = __builtin_amdgcn_ballot_w64(!out) & ((1ull << L) - 1ull);
+                sp_l = sp;                                          // lane j: move j's row slot
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             }
             while (pend) {
@@ -572,7 +574,7 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
                 const float2 qa = *(const float2*)slot;             // (qx, qy)
                 const float2 qb = *(const float2*)(slot + stride);  // (qz, T)
                 const float qx = qa.x, qy = qa.y, qz = qb.x, Tm = qb.y;
-                const int si = S_nb + ((i + j) >= n_own ? i + j - n_own : i + j);
+                const int si = __builtin_amdgcn_readlane(sp_l, j);  // S_nb + particle of move j
                 const float xi = px_[si], yi = py_[si], zi = pz_[si];
                 ++n_ev;
                 px_[si] = kFar;          // exclude the moving particle from its own term list
