@@ -73,14 +73,6 @@ __device__ __forceinline__ int mbcnt64_add(unsigned long long m, int add) {
 }
 __device__ __forceinline__ int mbcnt64(unsigned long long m) { return mbcnt64_add(m, 0); }
 
-// Per-lane select by a wave mask with both arms computed: the empty asm pins `a` in a VGPR, so
-// the compiler emits one v_cndmask instead of sinking a's computation into an exec-masked
-// branch (which costs ~5 scalar instructions of exec bookkeeping per select).
-__device__ __forceinline__ int select_by_mask(unsigned long long m, int a, int b) {
-    asm volatile("" : "+v"(a));
-    return __builtin_amdgcn_inverse_ballot_w64(m) ? a : b;
-}
-
 // pmc_lj4_signed_m with the r2 floor as ONE v_max_f32 (|r2s| is a free source modifier; the
 // compiler's fmaxf would add canonicalizing maxes, the C form a compare + select): identical
 // values for the non-NaN inputs of the term list (max(|r2s|, r2min) == (|r2s| < r2min ? r2min :
