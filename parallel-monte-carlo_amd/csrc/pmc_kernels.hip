@@ -742,6 +742,8 @@ __device__ __forceinline__ void subsweep_pair(const DevGeom& g, float* __restric
     float* buf = pz_ + stride;
     const int h = lane & 32;                       // 0: cell A's half, 32: cell B's
     const int l = lane & 31;
+    [[maybe_unused]] int t = tA;                   // (PMC_STAMP's cell index)
+    PMC_STAMP(0);
     const CellGeo ca = cell_geo(g, tA, cz0, ox, oy, oz);
     const CellGeo cb = cell_geo(g, hasB ? tA + 1 : tA, cz0, ox, oy, oz);
     // ---- stencil tables of both cells, counts ----------------------------------------------
@@ -754,8 +756,10 @@ __device__ __forceinline__ void subsweep_pair(const DevGeom& g, float* __restric
     const StencilLane sl = stencil_lane(g, cl, l, ca.edge || cb.edge);
     const int k_cnt = ncnt[sl.kc];
     const uint32_t k_off = sl.kc * (uint32_t)(3 * nm) * DiskAddr<OFF32>::kUnit;
+    PMC_STAMP(1);
     VisitLoads<NSLOT, NMC, OFF32> ld;
     ld.issue(g, disk, ca, k_off, 0);
+    PMC_STAMP(2);
     // ---- one RNG pass for both cells ---------------------------------------------------------
     const uint32_t idl = h ? cb.id : ca.id;
     uint32_t idx, tag;
@@ -793,13 +797,19 @@ __device__ __forceinline__ void subsweep_pair(const DevGeom& g, float* __restric
         }
     };
     park(0);
+    PMC_STAMP(3);
     if (!visit_cell<NSLOT, NMC, LCAP, OFF32, false>(g, disk, sweep, stats, px_, LCAP, cap, tA, ca, 0, k_cnt, k_off,
                                                     sl.sx, sl.sy, sl.sz, ld, jv, 16, 10, nullptr, 0)) {
         if (lane == 0) ovf[kOvfHead + atomicAdd(&ovf[kOvfCount], 1)] = tA;
     }
     if (!hasB) return;
+    t = tA + 1;
+    PMC_STAMP(0);
+    PMC_STAMP(1);
     park(32);
     ld.issue(g, disk, cb, k_off, 32);
+    PMC_STAMP(2);
+    PMC_STAMP(3);
     if (!visit_cell<NSLOT, NMC, LCAP, OFF32, false>(g, disk, sweep, stats, px_, LCAP, cap, tA + 1, cb, 32, k_cnt,
                                                     k_off, sl.sx, sl.sy, sl.sz, ld, jv, 16, 10, nullptr, 0)) {
         if (lane == 0) ovf[kOvfHead + atomicAdd(&ovf[kOvfCount], 1)] = tA + 1;
