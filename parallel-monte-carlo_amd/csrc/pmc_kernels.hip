@@ -726,17 +726,20 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
 //                          20 <= l < 30 -log u of move l-20
 // (h = 0 for A, 32 for B).  Cell A is visited with its rows loaded up front; B's randoms wait in
 // registers and its loads go out after A.
-template <int NSLOT, int NMC, bool OFF32>
+// LCAP = kMainCap for the main launch (overflowing cells go to `ovf`), 27*nmax for the slab
+// boundary launch (full capacity: nothing overflows, ovf unused; MIRROR rows as visit_cell).
+template <int NSLOT, int NMC, int LCAP, bool OFF32, bool MIRROR = false>
 __device__ __forceinline__ void subsweep_pair(const DevGeom& g, float* __restrict__ disk,
                                               const int16_t* __restrict__ ncnt, int ox, int oy, int oz,
                                               uint32_t sweep, unsigned long long* __restrict__ stats,
-                                              float* __restrict__ px_, int cap, int tA, bool hasB, int cz0,
-                                              int* __restrict__ ovf) {
-    constexpr int LCAP = kMainCap;
+                                              float* __restrict__ px_, int lcap_rt, int cap, int tA, bool hasB,
+                                              int cz0, int* __restrict__ ovf, float* __restrict__ mirror = nullptr,
+                                              int mirror_mode = 0) {
     const int lane = threadIdx.x & (kWave - 1);
     const int nm = NMC > 0 ? NMC : g.nmax;
-    constexpr int stride = subsweep_stride(LCAP);
-    constexpr int lcap4 = (LCAP + 3) & ~3;
+    const int lcap = LCAP > 0 ? LCAP : lcap_rt;
+    const int stride = subsweep_stride(lcap);
+    const int lcap4 = (lcap + 3) & ~3;
     float* py_ = px_ + stride;
     float* pz_ = py_ + stride;
     float* buf = pz_ + stride;
@@ -798,9 +801,9 @@ __device__ __forceinline__ void subsweep_pair(const DevGeom& g, float* __restric
     };
     park(0);
     PMC_STAMP(3);
-    if (!visit_cell<NSLOT, NMC, LCAP, OFF32, false>(g, disk, sweep, stats, px_, LCAP, cap, tA, ca, 0, k_cnt, k_off,
-                                                    sl.sx, sl.sy, sl.sz, ld, jv, 16, 10, nullptr, 0)) {
-        if (lane == 0) ovf[kOvfHead + atomicAdd(&ovf[kOvfCount], 1)] = tA;
+    if (!visit_cell<NSLOT, NMC, LCAP, OFF32, MIRROR>(g, disk, sweep, stats, px_, lcap, cap, tA, ca, 0, k_cnt, k_off,
+                                                     sl.sx, sl.sy, sl.sz, ld, jv, 16, 10, mirror, mirror_mode)) {
+        if (lane == 0 && ovf) ovf[kOvfHead + atomicAdd(&ovf[kOvfCount], 1)] = tA;
     }
     if (!hasB) return;
     t = tA + 1;
@@ -810,9 +813,9 @@ __device__ __forceinline__ void subsweep_pair(const DevGeom& g, float* __restric
     ld.issue(g, disk, cb, k_off, 32);
     PMC_STAMP(2);
     PMC_STAMP(3);
-    if (!visit_cell<NSLOT, NMC, LCAP, OFF32, false>(g, disk, sweep, stats, px_, LCAP, cap, tA + 1, cb, 32, k_cnt,
-                                                    k_off, sl.sx, sl.sy, sl.sz, ld, jv, 16, 10, nullptr, 0)) {
-        if (lane == 0) ovf[kOvfHead + atomicAdd(&ovf[kOvfCount], 1)] = tA + 1;
+    if (!visit_cell<NSLOT, NMC, LCAP, OFF32, MIRROR>(g, disk, sweep, stats, px_, lcap, cap, tA + 1, cb, 32, k_cnt,
+                                                     k_off, sl.sx, sl.sy, sl.sz, ld, jv, 16, 10, mirror, mirror_mode)) {
+        if (lane == 0 && ovf) ovf[kOvfHead + atomicAdd(&ovf[kOvfCount], 1)] = tA + 1;
     }
 }
 
@@ -839,7 +842,8 @@ __global__ __launch_bounds__(kWave * kSubWaves) __attribute__((amdgpu_waves_per_
     // two cells per wave (shared stencil table and RNG pass): wave w takes cells 2w and 2w+1
     const int t = 2 * ((int)b * kSubWaves + wv);
     if (t >= total) return;
-    subsweep_pair<NSLOT, NMC, OFF32>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, cap, t, t + 1 < total, cz0, ovf);
+    subsweep_pair<NSLOT, NMC, kMainCap, OFF32>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, kMainCap, cap, t,
+                                               t + 1 < total, cz0, ovf);
 #else
     const int t = (int)b * kSubWaves + wv;
     if (t >= total) return;
@@ -865,14 +869,14 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_direct(DevGeom g
     const int full = 27 * (NMC > 0 ? NMC : g.nmax);
     float* px_ = smem + wv * lds_floats_per_wave(full);
     const int total = (g.cps_x >> 1) * (g.cps_y >> 1) * ncz;
-    const int t = (int)blockIdx.x * kSubWaves + wv;
+    const int t = 2 * ((int)blockIdx.x * kSubWaves + wv);    // two cells per wave
     if (t >= total) return;
     if (mirror)
-        (void)subsweep_wave<NSLOT, NMC, 27 * NMC, OFF32, true>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, full,
-                                                               full, t, cz0, mirror, mirror_mode);
+        subsweep_pair<NSLOT, NMC, 27 * NMC, OFF32, true>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, full, full, t,
+                                                         t + 1 < total, cz0, nullptr, mirror, mirror_mode);
     else
-        (void)subsweep_wave<NSLOT, NMC, 27 * NMC, OFF32>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, full, full,
-                                                         t, cz0);
+        subsweep_pair<NSLOT, NMC, 27 * NMC, OFF32>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, full, full, t,
+                                                   t + 1 < total, cz0, nullptr);
 }
 
 // Fallback launch: full capacity (27*nmax partners per wave), a fixed grid striding over the
@@ -1235,7 +1239,7 @@ template <int NSLOT, int NMC, bool OFF32>
 static void launch_direct_t(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz, uint32_t sweep,
                             unsigned long long* stats, int cz0, int ncz, float* mirror, int mode, hipStream_t st) {
     const int64_t total = (int64_t)(g.cps_x / 2) * (g.cps_y / 2) * ncz;
-    const int64_t blocks = (total + kSubWaves - 1) / kSubWaves;
+    const int64_t blocks = ((total + 1) / 2 + kSubWaves - 1) / kSubWaves;   // two cells per wave
     const size_t lds = sizeof(float) * (size_t)lds_floats_per_wave(27 * g.nmax) * kSubWaves;
     hipLaunchKernelGGL((k_subsweep_direct<NSLOT, NMC, OFF32>), dim3((unsigned)blocks), dim3(kWave * kSubWaves), lds,
                        st, g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, mirror, mode);
