@@ -182,8 +182,8 @@ def main() -> int:
             if s not in plans:
                 plans[s] = sweep_plan(1234, s, 2.5)
             for colour in plans[s][0]:
-                timer("phase", lambda: sim.phase(colour, s), record)
-            timer("shift", lambda: sim.shift(s), record)
+                sim.phase(colour, s)
+            sim.shift(s)
 
         def finish():
             pass
@@ -243,8 +243,9 @@ def main() -> int:
     abytes = algorithmic_bytes_per_sweep(n_owned, stencil)
     e_start = sim.energy()      # cell-list energy of the state the timed region starts from
 
-    if c_slab:
-        sim.slab_timing(not args.no_events)    # per-launch HIP events inside the C driver
+    c_events = not slab or c_slab      # kernel launches from C: events on their dispatch packets
+    if c_events:
+        sim.timing(not args.no_events)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -265,8 +266,8 @@ def main() -> int:
     phase_total_ms = sum(a.elapsed_time(b) for kind, a, b in events if kind == "phase")
     shift_total_ms = sum(a.elapsed_time(b) for kind, a, b in events if kind == "shift")
     n_phases = 8 * args.steps if events else 0
-    if c_slab:
-        tm = sim.slab_timing(False)
+    if c_events:
+        tm = sim.timing(False)
         phase_total_ms, shift_total_ms = tm["subsweep_ms"], tm["shift_ms"]
         n_phases = 8 * args.steps if tm["n_subsweep"] else 0
     if world > 1:

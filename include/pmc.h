@@ -166,7 +166,11 @@ int pmc_slab_sweep(pmc_ctx* ctx, uint32_t sweep);
 /* Order the context stream after the outstanding exchanges (before reading state or halos). */
 int pmc_slab_finish(pmc_ctx* ctx);
 /* Sum of the HIP-event durations of the subsweep and shift launches since the last call
- * (synchronizes), then switch per-launch events on (enable = 1) or off. */
+ * (synchronizes), then switch per-launch events on (enable = 1) or off.  The events ride on the
+ * kernels' own dispatch packets (no extra packets between launches); graph replays are not timed.
+ * pmc_timing covers every launch of the context; pmc_slab_timing is the same call, requiring the
+ * slab driver. */
+int pmc_timing(pmc_ctx* ctx, int enable, double* subsweep_ms, int* n_subsweep, double* shift_ms, int* n_shift);
 int pmc_slab_timing(pmc_ctx* ctx, int enable, double* subsweep_ms, int* n_subsweep, double* shift_ms,
                     int* n_shift);
 /* The per-sweep plan every rank replicates (no broadcast): colour order (FY_Shuffle + itoa,

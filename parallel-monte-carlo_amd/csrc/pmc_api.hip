@@ -41,6 +41,10 @@ struct pmc_ctx {
     bool own_stream = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipGraphExec_t graph_exec = nullptr;
+    // per-launch kernel timing (pmc_timing): dispatch-packet events, (start, stop) pairs in use
+    bool timing = false;
+    std::vector<hipEvent_t> tev;
+    std::vector<int> tkind;                // 0 subsweep, 1 shift
     uint32_t graph_first = 0;
     int graph_count = 0;
     int graph_cur = -1;
@@ -142,17 +146,35 @@ void drop_graph(pmc_ctx* c) {
 
 void drop_slab(pmc_ctx* c);
 
+// the next timing slot when pmc_timing is on (nullptr otherwise): events ride on the launch's
+// dispatch packet (hipExtLaunchKernelGGL), no extra packets in the stream
+const LaunchTiming* next_timing(pmc_ctx* c, int kind, LaunchTiming* lt) {
+    if (!c->timing) return nullptr;
+    const size_t k = c->tkind.size();
+    while (c->tev.size() < 2 * (k + 1)) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        c->tev.push_back(e);
+    }
+    c->tkind.push_back(kind);
+    lt->start = c->tev[2 * k];
+    lt->stop = c->tev[2 * k + 1];
+    return lt;
+}
+
 int enqueue_sweep(pmc_ctx* c, uint32_t sweep) {
     const pmc_sweep_plan_t plan = pmc_plan_for_sweep(c->P.seed, sweep, c->P.w);
     for (int k = 0; k < 8; ++k) {
         int o[3];
         pmc_colour_offset(plan.order[k], o);
+        LaunchTiming lt;
         hipError_t e = launch_subsweep(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep,
-                                       c->stats, c->ovf, 0, c->P.nz_local, c->stream);
+                                       c->stats, c->ovf, 0, c->P.nz_local, c->stream, next_timing(c, 0, &lt));
         if (e != hipSuccess) return hip_fail(e, "subsweep launch");
     }
+    LaunchTiming lt;
     hipError_t e = launch_shift(c->G, c->disk[c->cur], c->n[c->cur], c->disk[c->cur ^ 1], c->n[c->cur ^ 1],
-                                plan.f, plan.d, c->flags, c->stream);
+                                plan.f, plan.d, c->flags, c->stream, next_timing(c, 1, &lt));
     if (e != hipSuccess) return hip_fail(e, "shift launch");
     c->cur ^= 1;
     return PMC_OK;
@@ -226,6 +248,7 @@ void pmc_destroy(pmc_ctx* c) {
     if (c->tmp_cnt) (void)hipFree(c->tmp_cnt);
     if (c->tmp_idx) (void)hipFree(c->tmp_idx);
     if (c->d_r) (void)hipFree(c->d_r);
+    for (hipEvent_t e : c->tev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
@@ -298,8 +321,9 @@ int pmc_subsweep_range(pmc_ctx* c, float* d_disk, const int16_t* d_n, const int 
         if (offset[k] != 0 && offset[k] != 1) return fail(PMC_ERR_ARG, "offset must be in {0,1}^3");
     if (zl_begin < 0 || zl_end > c->P.nz_local || zl_begin > zl_end)
         return fail(PMC_ERR_ARG, "plane range outside the owned planes");
+    LaunchTiming lt;
     hipError_t e = launch_subsweep(c->G, d_disk, d_n, offset[0], offset[1], offset[2], sweep, c->stats, c->ovf,
-                                   zl_begin, zl_end, c->stream);
+                                   zl_begin, zl_end, c->stream, next_timing(c, 0, &lt));
     return e == hipSuccess ? PMC_OK : hip_fail(e, "subsweep launch");
 }
 
@@ -313,7 +337,8 @@ int pmc_shift_cells(pmc_ctx* c, const float* din, const int16_t* nin, float* dou
     if (!c || !din || !nin || !dout || !nout) return fail(PMC_ERR_ARG, "null buffer");
     if (f < 0 || f > 2) return fail(PMC_ERR_ARG, "f must be 0, 1 or 2 (reference draws -1..1: start.cu:251)");
     if (din == dout || nin == nout) return fail(PMC_ERR_ARG, "shift is double-buffered: in != out");
-    hipError_t e = launch_shift(c->G, din, nin, dout, nout, f, d, c->flags, c->stream);
+    LaunchTiming lt;
+    hipError_t e = launch_shift(c->G, din, nin, dout, nout, f, d, c->flags, c->stream, next_timing(c, 1, &lt));
     return e == hipSuccess ? PMC_OK : hip_fail(e, "shift launch");
 }
 
@@ -392,8 +417,9 @@ int pmc_phase_range_on(pmc_ctx* c, int colour, uint32_t sweep, int zl_begin, int
     }
     int o[3];
     pmc_colour_offset(colour, o);
+    LaunchTiming lt;
     hipError_t e = launch_subsweep(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep, c->stats,
-                                   c->ovf_aux, zl_begin, zl_end, st);
+                                   c->ovf_aux, zl_begin, zl_end, st, next_timing(c, 0, &lt));
     return e == hipSuccess ? PMC_OK : hip_fail(e, "subsweep launch");
 }
 
@@ -428,11 +454,14 @@ int pmc_run_graph(pmc_ctx* c, uint32_t first, int count) {
         drop_graph(c);
         hipGraph_t graph = nullptr;
         const int cur0 = c->cur;
+        const bool timing = c->timing;   // no per-launch events inside a graph
+        c->timing = false;
         PMC_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
         int rc = PMC_OK;
         for (int k = 0; k < count && rc == PMC_OK; ++k) rc = enqueue_sweep(c, first + (uint32_t)k);
         hipError_t e = hipStreamEndCapture(c->stream, &graph);
         c->cur = cur0;
+        c->timing = timing;
         if (rc) { if (graph) (void)hipGraphDestroy(graph); return rc; }
         if (e != hipSuccess) return hip_fail(e, "hipStreamEndCapture");
         e = hipGraphInstantiate(&c->graph_exec, graph, nullptr, nullptr, 0);
@@ -746,9 +775,6 @@ struct pmc_slab {
     float* rbuf = nullptr;                // ... of the received plane
     size_t pack_floats = 0;
     int pend_colour = -1, pend_dst = 0;   // unpack owed on aux (colour, halo plane)
-    bool timing = false;                  // HIP events around every subsweep / shift launch
-    std::vector<hipEvent_t> tev;          // pool: (start, end) pairs
-    std::vector<int> tkind;               // 0 subsweep, 1 shift, per pair in use
 };
 
 namespace {
@@ -761,7 +787,6 @@ void drop_slab(pmc_ctx* c) {
     if (s->aux) (void)hipStreamDestroy(s->aux);
     for (hipEvent_t e : {s->ev_i, s->ev_b, s->ev_t})
         if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t e : s->tev) (void)hipEventDestroy(e);
     if (s->sbuf) (void)hipFree(s->sbuf);
     if (s->rbuf) (void)hipFree(s->rbuf);
     delete s;
@@ -774,24 +799,6 @@ size_t plane_cells(const pmc_ctx* c) { return (size_t)c->P.cps_x * c->P.cps_y; }
 float* disk_plane(pmc_ctx* c, int z) { return c->disk[c->cur] + (size_t)(z + 1) * plane_floats(c); }
 int16_t* n_plane(pmc_ctx* c, int z) { return c->n[c->cur] + (size_t)(z + 1) * plane_cells(c); }
 
-// one timed launch: events around `launch` on stream st when timing is on
-template <class F>
-hipError_t timed(pmc_slab* s, int kind, hipStream_t st, F&& launch) {
-    if (!s->timing) return launch();
-    const size_t k = s->tkind.size();
-    while (s->tev.size() < 2 * (k + 1)) {
-        hipEvent_t e;
-        hipError_t r = hipEventCreate(&e);
-        if (r != hipSuccess) return r;
-        s->tev.push_back(e);
-    }
-    s->tkind.push_back(kind);
-    hipError_t r = hipEventRecord(s->tev[2 * k], st);
-    if (r != hipSuccess) return r;
-    r = launch();
-    if (r != hipSuccess) return r;
-    return hipEventRecord(s->tev[2 * k + 1], st);
-}
 
 // finish the previous phase exchange on aux: unpack the received colour cells into the halo
 int slab_complete(pmc_ctx* c) {
@@ -948,10 +955,9 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
         PMC_HIP(hipStreamWaitEvent(T, s->ev_i, 0));            // I(k-1)
         if (k > 0) PMC_HIP(hipStreamWaitEvent(S, s->ev_b, 0)); // B(k-1)
         if (nz > 2) {
-            e = timed(s, 0, S, [&] {
-                return launch_subsweep(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep, c->stats,
-                                       c->ovf, 1, nz - 1, S);
-            });
+            LaunchTiming lt;
+            e = launch_subsweep(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep, c->stats, c->ovf, 1,
+                                nz - 1, S, next_timing(c, 0, &lt));
             if (e != hipSuccess) return hip_fail(e, "subsweep launch");
         }
         PMC_HIP(hipEventRecord(s->ev_i, S));
@@ -961,10 +967,9 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
         const bool down = o[2] == 0;
         const int zb = down ? 0 : nz - 1;
         float* mirror = s->comm ? s->sbuf : disk_plane(c, down ? nz : -1);
-        e = timed(s, 0, T, [&] {
-            return launch_subsweep_boundary(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep,
-                                            c->stats, zb, zb + 1, mirror, s->comm ? 0 : 1, T);
-        });
+        LaunchTiming lt;
+        e = launch_subsweep_boundary(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep, c->stats, zb,
+                                     zb + 1, mirror, s->comm ? 0 : 1, T, next_timing(c, 0, &lt));
         if (e != hipSuccess) return hip_fail(e, "subsweep launch");
         PMC_HIP(hipEventRecord(s->ev_b, T));
         if ((rc = slab_exchange_phase(c, colour))) return rc;
@@ -972,10 +977,9 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
     if ((rc = slab_complete(c))) return rc;
     PMC_HIP(hipEventRecord(s->ev_t, T));
     PMC_HIP(hipStreamWaitEvent(S, s->ev_t, 0));
-    e = timed(s, 1, S, [&] {
-        return launch_shift(c->G, c->disk[c->cur], c->n[c->cur], c->disk[c->cur ^ 1], c->n[c->cur ^ 1], plan.f,
-                            plan.d, c->flags, S);
-    });
+    LaunchTiming lts;
+    e = launch_shift(c->G, c->disk[c->cur], c->n[c->cur], c->disk[c->cur ^ 1], c->n[c->cur ^ 1], plan.f, plan.d,
+                     c->flags, S, next_timing(c, 1, &lts));
     if (e != hipSuccess) return hip_fail(e, "shift launch");
     c->cur ^= 1;
     // shiftCells moved particles across the boundary planes: refresh both halos with counts; the
@@ -994,19 +998,17 @@ int pmc_slab_finish(pmc_ctx* c) {
     return PMC_OK;
 }
 
-int pmc_slab_timing(pmc_ctx* c, int enable, double* subsweep_ms, int* n_subsweep, double* shift_ms,
-                    int* n_shift) {
-    if (!c || !c->slab) return fail(PMC_ERR_ARG, "no slab driver (pmc_slab_init)");
-    pmc_slab* s = c->slab;
+int pmc_timing(pmc_ctx* c, int enable, double* subsweep_ms, int* n_subsweep, double* shift_ms, int* n_shift) {
+    if (!c) return fail(PMC_ERR_ARG, "null ctx");
     double a = 0.0, b = 0.0;
     int na = 0, nb = 0;
-    if (!s->tkind.empty()) {
-        PMC_HIP(hipStreamSynchronize(s->aux));
+    if (!c->tkind.empty()) {
         PMC_HIP(hipStreamSynchronize(c->stream));
-        for (size_t k = 0; k < s->tkind.size(); ++k) {
+        if (c->slab) PMC_HIP(hipStreamSynchronize(c->slab->aux));
+        for (size_t k = 0; k < c->tkind.size(); ++k) {
             float ms = 0.0f;
-            PMC_HIP(hipEventElapsedTime(&ms, s->tev[2 * k], s->tev[2 * k + 1]));
-            if (s->tkind[k] == 0) { a += ms; ++na; }
+            PMC_HIP(hipEventElapsedTime(&ms, c->tev[2 * k], c->tev[2 * k + 1]));
+            if (c->tkind[k] == 0) { a += ms; ++na; }
             else { b += ms; ++nb; }
         }
     }
@@ -1014,9 +1016,15 @@ int pmc_slab_timing(pmc_ctx* c, int enable, double* subsweep_ms, int* n_subsweep
     if (n_subsweep) *n_subsweep = na;
     if (shift_ms) *shift_ms = b;
     if (n_shift) *n_shift = nb;
-    s->tkind.clear();
-    s->timing = enable != 0;
+    c->tkind.clear();
+    c->timing = enable != 0;
     return PMC_OK;
+}
+
+int pmc_slab_timing(pmc_ctx* c, int enable, double* subsweep_ms, int* n_subsweep, double* shift_ms,
+                    int* n_shift) {
+    if (!c || !c->slab) return fail(PMC_ERR_ARG, "no slab driver (pmc_slab_init)");
+    return pmc_timing(c, enable, subsweep_ms, n_subsweep, shift_ms, n_shift);
 }
 
 }  // extern "C"

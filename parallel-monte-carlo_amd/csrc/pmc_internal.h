@@ -52,21 +52,29 @@ struct DevGeom {
     uint32_t k0, k1;
 };
 
+// Optional timing of one kernel launch: start/stop events carried by the dispatch packet itself
+// (hipExtLaunchKernelGGL: no extra barrier packets between kernels, unlike hipEventRecord).
+struct LaunchTiming {
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+
 // Launchers (pmc_kernels.hip).  All asynchronous on `st`.
 // ovf: int[1 + cells_per_colour] scratch (overflow queue for the full-capacity fallback)
 // only cells in local planes [zl_begin, zl_end) of the colour are visited
 hipError_t launch_subsweep(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
                            uint32_t sweep, unsigned long long* stats, int* ovf, int zl_begin, int zl_end,
-                           hipStream_t st);
+                           hipStream_t st, const LaunchTiming* tm = nullptr);
 // the slab driver's boundary planes: full LDS capacity (no overflow queue), every written-back row
 // also stored to `mirror` (mirror_mode 0: packed colour rows ta + tb*cps_x/2, 1: plane rows;
 // mirror may be null)
 hipError_t launch_subsweep_boundary(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
                                     uint32_t sweep, unsigned long long* stats, int zl_begin, int zl_end,
-                                    float* mirror, int mirror_mode, hipStream_t st);
+                                    float* mirror, int mirror_mode, hipStream_t st,
+                                    const LaunchTiming* tm = nullptr);
 int subsweep_capacity(const DevGeom& g);
 hipError_t launch_shift(const DevGeom& g, const float* din, const int16_t* nin, float* dout,
-                        int16_t* nout, int f, float d, uint32_t* flags, hipStream_t st);
+                        int16_t* nout, int f, float d, uint32_t* flags, hipStream_t st,
+                        const LaunchTiming* tm = nullptr);
 hipError_t launch_init_r(const DevGeom& g, int64_t n_atoms, int64_t n_cube, float* r, hipStream_t st);
 hipError_t launch_assign(const DevGeom& g, const float* r, int64_t n_atoms, float* disk, int16_t* n,
                          int32_t* tmp_cnt, int32_t* tmp_idx, uint32_t* flags, hipStream_t st, int clip = 0);

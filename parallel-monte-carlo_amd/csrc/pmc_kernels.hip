@@ -17,6 +17,8 @@
 //
 // Build with -ffp-contract=off: every float/double op must stay a single IEEE op (the oracle,
 // compiled by gcc with the same flag, reproduces the results bit for bit).
+#include <hip/hip_ext.h>
+
 #include <cstdlib>
 #include <type_traits>
 
@@ -1198,6 +1200,13 @@ __global__ void k_selftest(const uint32_t* __restrict__ words, int count, float*
 // ------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------
+// hipLaunchKernelGGL, or with dispatch-packet timing events when tm is given
+template <class K, class... A>
+static void launch_k(K kernel, dim3 grid, dim3 block, size_t lds, hipStream_t st, const LaunchTiming* tm, A... args) {
+    if (tm && tm->start) hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)lds, st, tm->start, tm->stop, 0u, args...);
+    else hipLaunchKernelGGL(kernel, grid, block, lds, st, args...);
+}
+
 #ifndef PMC_FALLBACK_BLOCKS
 #define PMC_FALLBACK_BLOCKS 64   // fixed grid of the overflow launch (it strides over the queue)
 #endif
@@ -1219,15 +1228,15 @@ int subsweep_capacity(const DevGeom& g) {
 template <int NSLOT, int NMC, bool OFF32>
 static void launch_subsweep_t(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
                               uint32_t sweep, unsigned long long* stats, int* ovf, int cz0, int ncz,
-                              hipStream_t st) {
+                              hipStream_t st, const LaunchTiming* tm) {
     const int64_t total = (int64_t)(g.cps_x / 2) * (g.cps_y / 2) * ncz;
     const int64_t waves = (total + PMC_CELLS_PER_WAVE - 1) / PMC_CELLS_PER_WAVE;
     const int64_t blocks = (waves + kSubWaves - 1) / kSubWaves;
     const int cap = subsweep_capacity(g);
     const int full = 27 * g.nmax;
     const size_t lds = sizeof(float) * (size_t)lds_floats_per_wave(kMainCap) * kSubWaves;
-    hipLaunchKernelGGL((k_subsweep<NSLOT, NMC, OFF32>), dim3((unsigned)blocks), dim3(kWave * kSubWaves), lds, st, g,
-                       disk, n, ox, oy, oz, sweep, stats, cap, ovf, cz0, ncz);
+    launch_k(k_subsweep<NSLOT, NMC, OFF32>, dim3((unsigned)blocks), dim3(kWave * kSubWaves), lds, st, tm, g, disk, n,
+             ox, oy, oz, sweep, stats, cap, ovf, cz0, ncz);
     if (cap < full) {
         const size_t lds_full = sizeof(float) * (size_t)lds_floats_per_wave(full) * kSubWaves;
         hipLaunchKernelGGL((k_subsweep_fallback<NSLOT, NMC, OFF32>), dim3(PMC_FALLBACK_BLOCKS), dim3(kWave * kSubWaves), lds_full, st,
@@ -1237,54 +1246,55 @@ static void launch_subsweep_t(const DevGeom& g, float* disk, const int16_t* n, i
 
 template <int NSLOT, int NMC, bool OFF32>
 static void launch_direct_t(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz, uint32_t sweep,
-                            unsigned long long* stats, int cz0, int ncz, float* mirror, int mode, hipStream_t st) {
+                            unsigned long long* stats, int cz0, int ncz, float* mirror, int mode, hipStream_t st,
+                            const LaunchTiming* tm) {
     const int64_t total = (int64_t)(g.cps_x / 2) * (g.cps_y / 2) * ncz;
     const int64_t blocks = ((total + 1) / 2 + kSubWaves - 1) / kSubWaves;   // two cells per wave
     const size_t lds = sizeof(float) * (size_t)lds_floats_per_wave(27 * g.nmax) * kSubWaves;
-    hipLaunchKernelGGL((k_subsweep_direct<NSLOT, NMC, OFF32>), dim3((unsigned)blocks), dim3(kWave * kSubWaves), lds,
-                       st, g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, mirror, mode);
+    launch_k(k_subsweep_direct<NSLOT, NMC, OFF32>, dim3((unsigned)blocks), dim3(kWave * kSubWaves), lds, st, tm, g,
+             disk, n, ox, oy, oz, sweep, stats, cz0, ncz, mirror, mode);
 }
 
 template <bool OFF32>
 static void launch_direct_n(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz, uint32_t sweep,
-                            unsigned long long* stats, int cz0, int ncz, float* mirror, int mode, hipStream_t st) {
-    if (g.nmax == 16) launch_direct_t<16, 16, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, mirror, mode, st);
-    else if (g.nmax == 32) launch_direct_t<32, 32, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, mirror, mode, st);
-    else if (g.nslot == 8) launch_direct_t<8, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, mirror, mode, st);
-    else if (g.nslot == 16) launch_direct_t<16, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, mirror, mode, st);
-    else if (g.nslot == 32) launch_direct_t<32, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, mirror, mode, st);
-    else launch_direct_t<64, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, mirror, mode, st);
+                            unsigned long long* stats, int cz0, int ncz, float* mirror, int mode, hipStream_t st, const LaunchTiming* tm) {
+    if (g.nmax == 16) launch_direct_t<16, 16, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, mirror, mode, st, tm);
+    else if (g.nmax == 32) launch_direct_t<32, 32, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, mirror, mode, st, tm);
+    else if (g.nslot == 8) launch_direct_t<8, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, mirror, mode, st, tm);
+    else if (g.nslot == 16) launch_direct_t<16, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, mirror, mode, st, tm);
+    else if (g.nslot == 32) launch_direct_t<32, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, mirror, mode, st, tm);
+    else launch_direct_t<64, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, mirror, mode, st, tm);
 }
 
 template <bool OFF32>
 static void launch_subsweep_n(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
                               uint32_t sweep, unsigned long long* stats, int* ovf, int cz0, int ncz,
-                              hipStream_t st) {
-    if (g.nmax == 16) launch_subsweep_t<16, 16, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st);
-    else if (g.nmax == 32) launch_subsweep_t<32, 32, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st);
-    else if (g.nslot == 8) launch_subsweep_t<8, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st);
-    else if (g.nslot == 16) launch_subsweep_t<16, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st);
-    else if (g.nslot == 32) launch_subsweep_t<32, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st);
-    else launch_subsweep_t<64, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st);
+                              hipStream_t st, const LaunchTiming* tm) {
+    if (g.nmax == 16) launch_subsweep_t<16, 16, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st, tm);
+    else if (g.nmax == 32) launch_subsweep_t<32, 32, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st, tm);
+    else if (g.nslot == 8) launch_subsweep_t<8, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st, tm);
+    else if (g.nslot == 16) launch_subsweep_t<16, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st, tm);
+    else if (g.nslot == 32) launch_subsweep_t<32, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st, tm);
+    else launch_subsweep_t<64, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st, tm);
 }
 
 hipError_t launch_subsweep_boundary(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
                                     uint32_t sweep, unsigned long long* stats, int zl_begin, int zl_end,
-                                    float* mirror, int mirror_mode, hipStream_t st) {
+                                    float* mirror, int mirror_mode, hipStream_t st, const LaunchTiming* tm) {
     auto ceil_half = [](int v) { return v <= 0 ? 0 : (v + 1) / 2; };
     const int nczc = g.nz_local / 2;
     int cz0 = ceil_half(zl_begin - oz), cz1 = ceil_half(zl_end - oz);
     if (cz1 > nczc) cz1 = nczc;
     if (cz1 <= cz0) return hipSuccess;
     const int64_t bytes = (int64_t)g.cps_x * g.cps_y * (g.nz_local + 2 * g.halo) * 3 * g.nmax * 4;
-    if (bytes < ((int64_t)1 << 32)) launch_direct_n<true>(g, disk, n, ox, oy, oz, sweep, stats, cz0, cz1 - cz0, mirror, mirror_mode, st);
-    else launch_direct_n<false>(g, disk, n, ox, oy, oz, sweep, stats, cz0, cz1 - cz0, mirror, mirror_mode, st);
+    if (bytes < ((int64_t)1 << 32)) launch_direct_n<true>(g, disk, n, ox, oy, oz, sweep, stats, cz0, cz1 - cz0, mirror, mirror_mode, st, tm);
+    else launch_direct_n<false>(g, disk, n, ox, oy, oz, sweep, stats, cz0, cz1 - cz0, mirror, mirror_mode, st, tm);
     return hipGetLastError();
 }
 
 hipError_t launch_subsweep(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
                            uint32_t sweep, unsigned long long* stats, int* ovf, int zl_begin, int zl_end,
-                           hipStream_t st) {
+                           hipStream_t st, const LaunchTiming* tm) {
     // colour planes z = 2*cz + oz inside [zl_begin, zl_end)
     auto ceil_half = [](int v) { return v <= 0 ? 0 : (v + 1) / 2; };
     const int nczc = g.nz_local / 2;
@@ -1296,13 +1306,13 @@ hipError_t launch_subsweep(const DevGeom& g, float* disk, const int16_t* n, int 
     // (test hook: PMC_FORCE_ADDR64 takes the 64-bit path for any size)
     static const bool force64 = std::getenv("PMC_FORCE_ADDR64") != nullptr;
     const int64_t bytes = (int64_t)g.cps_x * g.cps_y * (g.nz_local + 2 * g.halo) * 3 * g.nmax * 4;
-    if (!force64 && bytes < ((int64_t)1 << 32)) launch_subsweep_n<true>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st);
-    else launch_subsweep_n<false>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st);
+    if (!force64 && bytes < ((int64_t)1 << 32)) launch_subsweep_n<true>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st, tm);
+    else launch_subsweep_n<false>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st, tm);
     return hipGetLastError();
 }
 
 hipError_t launch_shift(const DevGeom& g, const float* din, const int16_t* nin, float* dout,
-                        int16_t* nout, int f, float d, uint32_t* flags, hipStream_t st) {
+                        int16_t* nout, int f, float d, uint32_t* flags, hipStream_t st, const LaunchTiming* tm) {
 #ifndef PMC_SHIFT_U
 #define PMC_SHIFT_U 8
 #endif
@@ -1310,10 +1320,10 @@ hipError_t launch_shift(const DevGeom& g, const float* din, const int16_t* nin, 
     const int cpb = 256 / g.nslot;
     dim3 grid((unsigned)((g.cps_x + cpb * U - 1) / (cpb * U)), (unsigned)g.cps_y, (unsigned)g.nz_local), block(256);
     switch (g.nslot) {
-        case 8: hipLaunchKernelGGL((k_shift<8, U>), grid, block, 0, st, g, din, nin, dout, nout, f, d, flags); break;
-        case 16: hipLaunchKernelGGL((k_shift<16, U>), grid, block, 0, st, g, din, nin, dout, nout, f, d, flags); break;
-        case 32: hipLaunchKernelGGL((k_shift<32, U>), grid, block, 0, st, g, din, nin, dout, nout, f, d, flags); break;
-        default: hipLaunchKernelGGL((k_shift<64, U>), grid, block, 0, st, g, din, nin, dout, nout, f, d, flags); break;
+        case 8: launch_k(k_shift<8, U>, grid, block, 0, st, tm, g, din, nin, dout, nout, f, d, flags); break;
+        case 16: launch_k(k_shift<16, U>, grid, block, 0, st, tm, g, din, nin, dout, nout, f, d, flags); break;
+        case 32: launch_k(k_shift<32, U>, grid, block, 0, st, tm, g, din, nin, dout, nout, f, d, flags); break;
+        default: launch_k(k_shift<64, U>, grid, block, 0, st, tm, g, din, nin, dout, nout, f, d, flags); break;
     }
     return hipGetLastError();
 }

@@ -114,6 +114,7 @@ def lib():
         _sig(L, "pmc_slab_sweep", i32, _vp, u32)
         _sig(L, "pmc_slab_finish", i32, _vp)
         _sig(L, "pmc_slab_timing", i32, _vp, i32, _vp, _vp, _vp, _vp)
+        _sig(L, "pmc_timing", i32, _vp, i32, _vp, _vp, _vp, _vp)
         _sig(L, "pmc_subsweep_range", i32, _vp, _vp, _vp, C.POINTER(C.c_int * 3), u32, i32, i32)
         _sig(L, "pmc_shift", i32, _vp, u32)
         _sig(L, "pmc_start", i32, _vp, u32, i32, C.POINTER(Result))

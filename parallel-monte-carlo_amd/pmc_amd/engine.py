@@ -173,12 +173,19 @@ class PmcContext:
     def slab_finish(self) -> None:
         check("pmc_slab_finish", lib().pmc_slab_finish(self._h))
 
-    def slab_timing(self, enable: bool) -> dict:
+    def _timing(self, fn: str, enable: bool) -> dict:
         a, b = C.c_double(), C.c_double()
         na, nb = C.c_int(), C.c_int()
-        check("pmc_slab_timing", lib().pmc_slab_timing(self._h, int(enable), C.byref(a), C.byref(na), C.byref(b),
-                                                       C.byref(nb)))
+        check(fn, getattr(lib(), fn)(self._h, int(enable), C.byref(a), C.byref(na), C.byref(b), C.byref(nb)))
         return {"subsweep_ms": a.value, "n_subsweep": na.value, "shift_ms": b.value, "n_shift": nb.value}
+
+    def timing(self, enable: bool) -> dict:
+        """Summed kernel durations (dispatch-packet HIP events) of the subsweep / shift launches
+        since the last call; then per-launch timing on or off (pmc_timing)."""
+        return self._timing("pmc_timing", enable)
+
+    def slab_timing(self, enable: bool) -> dict:
+        return self._timing("pmc_slab_timing", enable)
 
     def shift(self, s: int) -> None:
         check("pmc_shift", lib().pmc_shift(self._h, s))
