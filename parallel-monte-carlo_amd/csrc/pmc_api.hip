@@ -856,6 +856,29 @@ int slab_exchange_full(pmc_ctx* c) {
     return PMC_OK;
 }
 
+// after a shift along z in direction dir: the halo on the +dir side takes the neighbour's new
+// plane next to it (the -dir side was shifted locally), on aux
+int slab_exchange_zplane(pmc_ctx* c, int dir) {
+    pmc_slab* s = c->slab;
+    const int nz = c->P.nz_local;
+    const size_t pf = plane_floats(c), pc = plane_cells(c);
+    const int src = dir > 0 ? 0 : nz - 1, dst = dir > 0 ? nz : -1;   // my plane -> the -dir rank's halo
+    if (!s->comm) {
+        PMC_HIP(hipMemcpyAsync(disk_plane(c, dst), disk_plane(c, src), pf * 4, hipMemcpyDeviceToDevice, s->aux));
+        PMC_HIP(hipMemcpyAsync(n_plane(c, dst), n_plane(c, src), pc * 2, hipMemcpyDeviceToDevice, s->aux));
+        return PMC_OK;
+    }
+    const int to = dir > 0 ? s->below : s->above, from = dir > 0 ? s->above : s->below;
+    Rccl& R = rccl();
+    PMC_NCCL(R.group_start());
+    PMC_NCCL(R.send(disk_plane(c, src), pf, ncclFloat32, to, s->comm, s->aux));
+    PMC_NCCL(R.send(n_plane(c, src), pc * 2, ncclUint8, to, s->comm, s->aux));
+    PMC_NCCL(R.recv(disk_plane(c, dst), pf, ncclFloat32, from, s->comm, s->aux));
+    PMC_NCCL(R.recv(n_plane(c, dst), pc * 2, ncclUint8, from, s->comm, s->aux));
+    PMC_NCCL(R.group_end());
+    return PMC_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -942,18 +965,26 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
     hipError_t e;
     int rc;
     // Per colour k:  S: wait B(k-1) -> interior I(k) = planes [1, nz-1) (reads no halo)
-    //                T: wait I(k-1) -> unpack halo of exchange k-1 -> boundary B(k) = the one
-    //                   boundary plane of parity oz -> pack + RCCL send/recv of its colour cells.
+    //                T: wait I(k-1) -> boundary B(k) = the one boundary plane of parity oz ->
+    //                   RCCL send/recv of its colour cells (packed by B(k)) -> unpack into the halo.
     // I(k) and B(k) run together; exchange k overlaps I(k+1).  I(k) never writes a plane an
     // exchange reads, nor reads a halo one writes.  Cells of a colour are independent, so any
     // split of a phase gives the whole-box result bit for bit.
+    // The cross-stream waits are only needed when the z parity changes: a phase of parity p
+    // writes planes of parity p and reads its own plane and the planes of parity 1-p, so I(k) and
+    // B(k-1) (or B(k) and I(k-1)) of equal parity touch disjoint planes.  The wait at the start of
+    // a run of equal parities orders it after every earlier phase of the other parity.
     PMC_HIP(hipEventRecord(s->ev_i, S));                       // "I(-1)": all earlier S work
+    int prev_oz = -1;
     for (int k = 0; k < 8; ++k) {
         const int colour = plan.order[k];
         int o[3];
         pmc_colour_offset(colour, o);
-        PMC_HIP(hipStreamWaitEvent(T, s->ev_i, 0));            // I(k-1)
-        if (k > 0) PMC_HIP(hipStreamWaitEvent(S, s->ev_b, 0)); // B(k-1)
+        if (o[2] != prev_oz) {
+            PMC_HIP(hipStreamWaitEvent(T, s->ev_i, 0));            // I(k-1)
+            if (k > 0) PMC_HIP(hipStreamWaitEvent(S, s->ev_b, 0)); // B(k-1)
+        }
+        prev_oz = o[2];
         if (nz > 2) {
             LaunchTiming lt;
             e = launch_subsweep(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep, c->stats, c->ovf, 1,
@@ -961,7 +992,6 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
             if (e != hipSuccess) return hip_fail(e, "subsweep launch");
         }
         PMC_HIP(hipEventRecord(s->ev_i, S));
-        if ((rc = slab_complete(c))) return rc;
         // the boundary plane of this parity, full capacity (no fallback launch); its written-back
         // rows go straight to the send buffer (RCCL) or to the periodic halo (single rank)
         const bool down = o[2] == 0;
@@ -972,21 +1002,35 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
                                      zb + 1, mirror, s->comm ? 0 : 1, T, next_timing(c, 0, &lt));
         if (e != hipSuccess) return hip_fail(e, "subsweep launch");
         PMC_HIP(hipEventRecord(s->ev_b, T));
+        // exchange k and its unpack follow B(k) on T straight away, so they run beside I(k)
+        // instead of between the wait for I(k) and B(k+1)
         if ((rc = slab_exchange_phase(c, colour))) return rc;
+        if ((rc = slab_complete(c))) return rc;
     }
     if ((rc = slab_complete(c))) return rc;
     PMC_HIP(hipEventRecord(s->ev_t, T));
     PMC_HIP(hipStreamWaitEvent(S, s->ev_t, 0));
+    // shiftCells: after the 8 phases both halo planes are exact copies of the
+    // neighbours' planes, so every halo plane whose new content depends only on planes this rank
+    // holds is shifted here, bit-identical to its owner's result.  Along x or y that is both halo
+    // planes (no exchange at all); along z in direction dir, the halo on the -dir side (it takes
+    // particles from the owned plane next to it), and the other one is received: one plane with
+    // its counts, one direction, instead of both planes.
+    const int dir = plan.d <= 0.0f ? -1 : 1;   // k_shift / shiftCells.h:46-53
+    int zl0 = -1, zl1 = nz + 1;
+    if (plan.f == 2) (dir > 0 ? zl1 : zl0) = dir > 0 ? nz : 0;
     LaunchTiming lts;
-    e = launch_shift(c->G, c->disk[c->cur], c->n[c->cur], c->disk[c->cur ^ 1], c->n[c->cur ^ 1], plan.f, plan.d,
-                     c->flags, S, next_timing(c, 1, &lts));
+    e = launch_shift_planes(c->G, c->disk[c->cur], c->n[c->cur], c->disk[c->cur ^ 1], c->n[c->cur ^ 1], plan.f,
+                            plan.d, c->flags, zl0, zl1, S, next_timing(c, 1, &lts));
     if (e != hipSuccess) return hip_fail(e, "shift launch");
     c->cur ^= 1;
-    // shiftCells moved particles across the boundary planes: refresh both halos with counts; the
-    // next sweep's first interior overlaps it, its first boundary launch follows it on T
-    PMC_HIP(hipEventRecord(s->ev_i, S));
-    PMC_HIP(hipStreamWaitEvent(T, s->ev_i, 0));
-    if ((rc = slab_exchange_full(c))) return rc;
+    // the next sweep's first boundary launch follows the shift on T ("I(-1)" wait); its first
+    // interior reads no halo, so it overlaps the z exchange
+    if (plan.f == 2) {
+        PMC_HIP(hipEventRecord(s->ev_i, S));
+        PMC_HIP(hipStreamWaitEvent(T, s->ev_i, 0));
+        if ((rc = slab_exchange_zplane(c, dir))) return rc;
+    }
     PMC_HIP(hipEventRecord(s->ev_t, T));
     return PMC_OK;
 }

@@ -75,6 +75,10 @@ int subsweep_capacity(const DevGeom& g);
 hipError_t launch_shift(const DevGeom& g, const float* din, const int16_t* nin, float* dout,
                         int16_t* nout, int f, float d, uint32_t* flags, hipStream_t st,
                         const LaunchTiming* tm = nullptr);
+// the same over local planes [zl_begin, zl_end), halo planes included (-halo .. nz_local+halo)
+hipError_t launch_shift_planes(const DevGeom& g, const float* din, const int16_t* nin, float* dout,
+                               int16_t* nout, int f, float d, uint32_t* flags, int zl_begin, int zl_end,
+                               hipStream_t st, const LaunchTiming* tm);
 hipError_t launch_init_r(const DevGeom& g, int64_t n_atoms, int64_t n_cube, float* r, hipStream_t st);
 hipError_t launch_assign(const DevGeom& g, const float* r, int64_t n_atoms, float* disk, int16_t* n,
                          int32_t* tmp_cnt, int32_t* tmp_idx, uint32_t* flags, hipStream_t st, int clip = 0);

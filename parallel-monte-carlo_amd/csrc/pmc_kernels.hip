@@ -919,14 +919,16 @@ template <int NSLOT, int U>
 __global__ __launch_bounds__(256) void k_shift(DevGeom g, const float* __restrict__ din,
                                                const int16_t* __restrict__ nin, float* __restrict__ dout,
                                                int16_t* __restrict__ nout, int f, float d,
-                                               uint32_t* __restrict__ flags) {
-    // grid: (ceil(cps_x / (CPB*U)), cps_y, nz_local); NSLOT lanes per cell, CPB cells per block
+                                               uint32_t* __restrict__ flags, int zl0) {
+    // grid: (ceil(cps_x / (CPB*U)), cps_y, planes); local plane zl = zl0 + blockIdx.z (zl0 = -1
+    // takes the bottom halo plane of a slab: the slab driver shifts the halo planes it can compute
+    // from its own data instead of receiving them).  NSLOT lanes per cell, CPB cells per block
     // along x per unrolled step j, U steps whose loads are all issued before any use (U times
     // the bytes in flight per wave: the kernel is latency-bound at one cell per lane group)
     constexpr int CPB = 256 / NSLOT;
     const int lane = threadIdx.x & (kWave - 1);
     const int p = threadIdx.x & (NSLOT - 1);
-    const int y = (int)blockIdx.y, zl = (int)blockIdx.z;
+    const int y = (int)blockIdx.y, zl = zl0 + (int)blockIdx.z;
     const int nm = g.nmax;
     const float w = g.w;
     const int cps_f = f == 0 ? g.cps_x : (f == 1 ? g.cps_y : g.cps_z);
@@ -948,7 +950,8 @@ __global__ __launch_bounds__(256) void k_shift(DevGeom g, const float* __restric
         const int x = ((int)blockIdx.x * U + j) * CPB + (int)(threadIdx.x / NSLOT);
         live[j] = x < g.cps_x;
         const int xx = live[j] ? x : 0;
-        const int cidf = f == 0 ? xx : (f == 1 ? y : g.z0 + zl);
+        int cidf = f == 0 ? xx : (f == 1 ? y : g.z0 + zl);
+        if (cidf < 0) cidf += cps_f; else if (cidf >= cps_f) cidf -= cps_f;   // halo planes wrap
         offset[j] = (float)cidf * w - Lf / 2.0f;           // :55
         int nbg = cidf + dir;
         if (nbg < 0) nbg = cps_f - 1; else if (nbg >= cps_f) nbg = 0;
@@ -1313,17 +1316,25 @@ hipError_t launch_subsweep(const DevGeom& g, float* disk, const int16_t* n, int 
 
 hipError_t launch_shift(const DevGeom& g, const float* din, const int16_t* nin, float* dout,
                         int16_t* nout, int f, float d, uint32_t* flags, hipStream_t st, const LaunchTiming* tm) {
+    return launch_shift_planes(g, din, nin, dout, nout, f, d, flags, 0, g.nz_local, st, tm);
+}
+
+hipError_t launch_shift_planes(const DevGeom& g, const float* din, const int16_t* nin, float* dout,
+                               int16_t* nout, int f, float d, uint32_t* flags, int zl_begin, int zl_end,
+                               hipStream_t st, const LaunchTiming* tm) {
+    if (zl_begin < -g.halo || zl_end > g.nz_local + g.halo || zl_end <= zl_begin) return hipErrorInvalidValue;
 #ifndef PMC_SHIFT_U
 #define PMC_SHIFT_U 8
 #endif
     constexpr int U = PMC_SHIFT_U;   // cells per lane group, loads hoisted
     const int cpb = 256 / g.nslot;
-    dim3 grid((unsigned)((g.cps_x + cpb * U - 1) / (cpb * U)), (unsigned)g.cps_y, (unsigned)g.nz_local), block(256);
+    dim3 grid((unsigned)((g.cps_x + cpb * U - 1) / (cpb * U)), (unsigned)g.cps_y, (unsigned)(zl_end - zl_begin)), block(256);
+    const int z0 = zl_begin;
     switch (g.nslot) {
-        case 8: launch_k(k_shift<8, U>, grid, block, 0, st, tm, g, din, nin, dout, nout, f, d, flags); break;
-        case 16: launch_k(k_shift<16, U>, grid, block, 0, st, tm, g, din, nin, dout, nout, f, d, flags); break;
-        case 32: launch_k(k_shift<32, U>, grid, block, 0, st, tm, g, din, nin, dout, nout, f, d, flags); break;
-        default: launch_k(k_shift<64, U>, grid, block, 0, st, tm, g, din, nin, dout, nout, f, d, flags); break;
+        case 8: launch_k(k_shift<8, U>, grid, block, 0, st, tm, g, din, nin, dout, nout, f, d, flags, z0); break;
+        case 16: launch_k(k_shift<16, U>, grid, block, 0, st, tm, g, din, nin, dout, nout, f, d, flags, z0); break;
+        case 32: launch_k(k_shift<32, U>, grid, block, 0, st, tm, g, din, nin, dout, nout, f, d, flags, z0); break;
+        default: launch_k(k_shift<64, U>, grid, block, 0, st, tm, g, din, nin, dout, nout, f, d, flags, z0); break;
     }
     return hipGetLastError();
 }

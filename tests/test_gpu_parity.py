@@ -324,20 +324,30 @@ def test_gpu_init_lattice_global_slab_planes(pmc, oracle):
 def test_gpu_c_slab_driver_equals_whole_box(pmc, oracle, nz, atoms, rccl):
     """The C slab driver (pmc_slab_*: two streams, colour-packed halo exchange; with rccl=True
     through a one-rank RCCL communicator sending to itself, the multi-GPU transport path) equals
-    the whole-box run bit for bit: every occupied slot, counts, counters and the energy."""
+    the whole-box run bit for bit: every occupied slot, counts, counters and the energy.
+    Sweeps 10-17 shift along x and y (10-12: both halo planes shifted locally) and along z in
+    both directions (13-17: one halo plane shifted locally, the other received); after the last
+    one both halo planes must equal the periodic images of the owned boundary planes."""
     import torch
     from pmc_amd.slab import SlabDriver
     drv = SlabDriver(cps=16, nz_local=nz, rank=0, world=1, atoms_per_rank=atoms, use_rccl=rccl)
     whole = pmc.PmcContext(16, cps_z=nz)
     whole.init_lattice(atoms)
-    drv.run(0, 4)
-    for s in range(4):
+    drv.run(10, 8)
+    for s in range(10, 18):
         whole.sweep(s)
     torch.cuda.synchronize()
     d_slab, n_slab = drv.owned()
     disk, n = whole.copy_out()
     assert np.array_equal(n_slab, n)
     assert oracle.valid_slots_equal(d_slab, n_slab, disk, n, 16)
+    d_all, n_all = drv.ctx.copy_out()
+    plane, row = 16 * 16, 3 * 16
+    d_all = d_all.reshape(nz + 2, plane * row)
+    n_all = n_all.reshape(nz + 2, plane)
+    for halo, image in ((0, nz), (nz + 1, 1)):
+        assert np.array_equal(n_all[halo], n_all[image])
+        assert oracle.valid_slots_equal(d_all[halo], n_all[halo], d_all[image], n_all[image], 16)
     assert drv.ctx.stats() == whole.stats()
     assert drv.ctx.error_flags() == 0
     assert drv.ctx.energy() == pytest.approx(whole.energy(), rel=1e-12, abs=1e-9)
