@@ -267,6 +267,43 @@ print("ok", r["accepted"])
     assert out.stdout.startswith("ok")
 
 
+@pytest.mark.parametrize("rccl", [False, True])
+def test_gpu_c_slab_driver_forced_fallback(rccl):
+    """PMC_SUBSWEEP_CAP=64 sends (almost) every cell of the C slab driver's interior launches to
+    the overflow queue and its fallback launch, beside the boundary launches on the aux stream.
+    Bit-identical to the whole box over x/y/z shifts.  Subprocess: the hook is read once."""
+    import os
+    import subprocess
+    import sys
+    code = r'''
+import sys, numpy as np
+sys.path[:0] = [sys.argv[1], sys.argv[2]]
+import torch, pmc_amd, pmc_oracle
+from pmc_amd.slab import SlabDriver
+rccl = sys.argv[3] == "1"
+drv = SlabDriver(cps=16, nz_local=8, rank=0, world=1, atoms_per_rank=5000, use_rccl=rccl)
+whole = pmc_amd.PmcContext(16, cps_z=8)
+whole.init_lattice(5000)
+drv.run(11, 6)
+for s in range(11, 17):
+    whole.sweep(s)
+torch.cuda.synchronize()
+d_slab, n_slab = drv.owned()
+disk, n = whole.copy_out()
+assert np.array_equal(n_slab, n)
+assert pmc_oracle.valid_slots_equal(d_slab, n_slab, disk, n, 16)
+assert drv.ctx.stats() == whole.stats()
+assert drv.ctx.error_flags() == 0
+print("ok", drv.ctx.stats())
+'''
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", code, os.path.join(repo, "parallel-monte-carlo_amd"),
+                          os.path.join(repo, "oracle"), "1" if rccl else "0"],
+                         env=dict(os.environ, PMC_SUBSWEEP_CAP="64"), capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert any(line.startswith("ok") for line in out.stdout.splitlines()), out.stdout[-2000:]   # (RCCL may print too)
+
+
 @pytest.mark.parametrize("nz,atoms,two_streams", [(16, 10_000, True), (16, 10_000, False), (4, 2_500, True)])
 def test_gpu_slab_single_rank_equals_whole_box(pmc, nz, atoms, two_streams):
     """The HIP slab path (halo planes, global z images, plane exchange through torch tensors)
