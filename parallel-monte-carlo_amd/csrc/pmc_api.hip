@@ -919,6 +919,12 @@ int pmc_slab_init(pmc_ctx* c, int rank, int world, const unsigned char* id) {
             return hip_fail(e, "hipEventCreate");
         }
     s->pack_floats = (size_t)(c->P.cps_x / 2) * (c->P.cps_y / 2) * 3 * c->P.nmax;
+    if (!c->ovf_aux) {   // the boundary launches' overflow queue (they run beside the interior's)
+        if ((e = hipMalloc(&c->ovf_aux, c->ovf_bytes)) != hipSuccess || (e = hipMemset(c->ovf_aux, 0, c->ovf_bytes)) != hipSuccess) {
+            drop_slab(c);
+            return hip_fail(e, "hipMalloc overflow queue");
+        }
+    }
     if (id) {
         Rccl& R = rccl();
         if (!R.ok) {
@@ -998,7 +1004,7 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
         const int zb = down ? 0 : nz - 1;
         float* mirror = s->comm ? s->sbuf : disk_plane(c, down ? nz : -1);
         LaunchTiming lt;
-        e = launch_subsweep_boundary(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep, c->stats, zb,
+        e = launch_subsweep_boundary(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep, c->stats, c->ovf_aux, zb,
                                      zb + 1, mirror, s->comm ? 0 : 1, T, next_timing(c, 0, &lt));
         if (e != hipSuccess) return hip_fail(e, "subsweep launch");
         PMC_HIP(hipEventRecord(s->ev_b, T));

@@ -68,7 +68,7 @@ hipError_t launch_subsweep(const DevGeom& g, float* disk, const int16_t* n, int 
 // also stored to `mirror` (mirror_mode 0: packed colour rows ta + tb*cps_x/2, 1: plane rows;
 // mirror may be null)
 hipError_t launch_subsweep_boundary(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
-                                    uint32_t sweep, unsigned long long* stats, int zl_begin, int zl_end,
+                                    uint32_t sweep, unsigned long long* stats, int* ovf, int zl_begin, int zl_end,
                                     float* mirror, int mirror_mode, hipStream_t st,
                                     const LaunchTiming* tm = nullptr);
 int subsweep_capacity(const DevGeom& g);

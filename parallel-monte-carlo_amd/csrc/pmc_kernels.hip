@@ -856,39 +856,43 @@ __global__ __launch_bounds__(kWave * kSubWaves) __attribute__((amdgpu_waves_per_
 #endif
 }
 
-// Boundary-plane launch of the slab driver: full capacity (27*nmax partners per wave: no overflow
-// queue, no fallback launch -- a plane is a small launch, occupancy is not what bounds it), one wave
-// per cell of the plane range, written-back rows mirrored into the halo exchange buffer.
+// Boundary-plane launch of the slab driver: the main launch's two-cell waves and capacity (5 KiB of
+// LDS per wave: its waves wait for the interior's to retire and then stay resident as long as the
+// interior runs, so they must not hold more LDS than an interior wave), written-back rows mirrored
+// into the halo exchange buffer; cells over the capacity go to its own queue, which a mirroring
+// fallback launch on the same stream visits.
 template <int NSLOT, int NMC, bool OFF32>
 __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_direct(DevGeom g, float* __restrict__ disk,
                                                                          const int16_t* __restrict__ ncnt,
                                                                          int ox, int oy, int oz, uint32_t sweep,
                                                                          unsigned long long* __restrict__ stats,
-                                                                         int cz0, int ncz, float* __restrict__ mirror,
+                                                                         int cap, int* __restrict__ ovf, int cz0,
+                                                                         int ncz, float* __restrict__ mirror,
                                                                          int mirror_mode) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int full = 27 * (NMC > 0 ? NMC : g.nmax);
-    float* px_ = smem + wv * lds_floats_per_wave(full);
+    float* px_ = smem + wv * lds_floats_per_wave(kMainCap);
     const int total = (g.cps_x >> 1) * (g.cps_y >> 1) * ncz;
     const int t = 2 * ((int)blockIdx.x * kSubWaves + wv);    // two cells per wave
     if (t >= total) return;
     if (mirror)
-        subsweep_pair<NSLOT, NMC, 27 * NMC, OFF32, true>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, full, full, t,
-                                                         t + 1 < total, cz0, nullptr, mirror, mirror_mode);
+        subsweep_pair<NSLOT, NMC, kMainCap, OFF32, true>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, kMainCap, cap, t,
+                                                         t + 1 < total, cz0, ovf, mirror, mirror_mode);
     else
-        subsweep_pair<NSLOT, NMC, 27 * NMC, OFF32>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, full, full, t,
-                                                   t + 1 < total, cz0, nullptr);
+        subsweep_pair<NSLOT, NMC, kMainCap, OFF32>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, kMainCap, cap, t,
+                                                   t + 1 < total, cz0, ovf);
 }
 
 // Fallback launch: full capacity (27*nmax partners per wave), a fixed grid striding over the
 // queued cells.  Cells of one colour are independent, so the order does not matter.
-template <int NSLOT, int NMC, bool OFF32>
+template <int NSLOT, int NMC, bool OFF32, bool MIRROR = false>
 __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_fallback(DevGeom g, float* __restrict__ disk,
                                                                            const int16_t* __restrict__ ncnt,
                                                                            int ox, int oy, int oz, uint32_t sweep,
                                                                            unsigned long long* __restrict__ stats,
-                                                                           int* __restrict__ ovf, int cz0) {
+                                                                           int* __restrict__ ovf, int cz0,
+                                                                           float* __restrict__ mirror = nullptr,
+                                                                           int mirror_mode = 0) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int full = 27 * (NMC > 0 ? NMC : g.nmax);
@@ -896,8 +900,8 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_fallback(DevGeom
     const int count = __builtin_amdgcn_readfirstlane(ovf[kOvfCount]);
     for (int e = (int)blockIdx.x * kSubWaves + wv; e < count; e += (int)gridDim.x * kSubWaves) {
         const int t = __builtin_amdgcn_readfirstlane(ovf[kOvfHead + e]);
-        (void)subsweep_wave<NSLOT, NMC, 27 * NMC, OFF32>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, full, full, t,
-                                                  cz0);
+        (void)subsweep_wave<NSLOT, NMC, 27 * NMC, OFF32, MIRROR>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, full,
+                                                                 full, t, cz0, mirror, mirror_mode);
     }
     // the last workgroup to finish (every workgroup has read the count by then) clears the queue
     // for the next launch: no memset between launches, and graph replays start from a clean queue
@@ -1249,24 +1253,37 @@ static void launch_subsweep_t(const DevGeom& g, float* disk, const int16_t* n, i
 
 template <int NSLOT, int NMC, bool OFF32>
 static void launch_direct_t(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz, uint32_t sweep,
-                            unsigned long long* stats, int cz0, int ncz, float* mirror, int mode, hipStream_t st,
-                            const LaunchTiming* tm) {
+                            unsigned long long* stats, int* ovf, int cz0, int ncz, float* mirror, int mode,
+                            hipStream_t st, const LaunchTiming* tm) {
     const int64_t total = (int64_t)(g.cps_x / 2) * (g.cps_y / 2) * ncz;
     const int64_t blocks = ((total + 1) / 2 + kSubWaves - 1) / kSubWaves;   // two cells per wave
-    const size_t lds = sizeof(float) * (size_t)lds_floats_per_wave(27 * g.nmax) * kSubWaves;
+    const int cap = subsweep_capacity(g);
+    const int full = 27 * g.nmax;
+    const size_t lds = sizeof(float) * (size_t)lds_floats_per_wave(kMainCap) * kSubWaves;
     launch_k(k_subsweep_direct<NSLOT, NMC, OFF32>, dim3((unsigned)blocks), dim3(kWave * kSubWaves), lds, st, tm, g,
-             disk, n, ox, oy, oz, sweep, stats, cz0, ncz, mirror, mode);
+             disk, n, ox, oy, oz, sweep, stats, cap, ovf, cz0, ncz, mirror, mode);
+    if (cap < full) {
+        const size_t lds_full = sizeof(float) * (size_t)lds_floats_per_wave(full) * kSubWaves;
+        if (mirror)
+            hipLaunchKernelGGL((k_subsweep_fallback<NSLOT, NMC, OFF32, true>), dim3(PMC_FALLBACK_BLOCKS),
+                               dim3(kWave * kSubWaves), lds_full, st, g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0,
+                               mirror, mode);
+        else
+            hipLaunchKernelGGL((k_subsweep_fallback<NSLOT, NMC, OFF32>), dim3(PMC_FALLBACK_BLOCKS),
+                               dim3(kWave * kSubWaves), lds_full, st, g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0,
+                               nullptr, 0);
+    }
 }
 
 template <bool OFF32>
 static void launch_direct_n(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz, uint32_t sweep,
-                            unsigned long long* stats, int cz0, int ncz, float* mirror, int mode, hipStream_t st, const LaunchTiming* tm) {
-    if (g.nmax == 16) launch_direct_t<16, 16, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, mirror, mode, st, tm);
-    else if (g.nmax == 32) launch_direct_t<32, 32, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, mirror, mode, st, tm);
-    else if (g.nslot == 8) launch_direct_t<8, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, mirror, mode, st, tm);
-    else if (g.nslot == 16) launch_direct_t<16, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, mirror, mode, st, tm);
-    else if (g.nslot == 32) launch_direct_t<32, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, mirror, mode, st, tm);
-    else launch_direct_t<64, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, mirror, mode, st, tm);
+                            unsigned long long* stats, int* ovf, int cz0, int ncz, float* mirror, int mode, hipStream_t st, const LaunchTiming* tm) {
+    if (g.nmax == 16) launch_direct_t<16, 16, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, mirror, mode, st, tm);
+    else if (g.nmax == 32) launch_direct_t<32, 32, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, mirror, mode, st, tm);
+    else if (g.nslot == 8) launch_direct_t<8, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, mirror, mode, st, tm);
+    else if (g.nslot == 16) launch_direct_t<16, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, mirror, mode, st, tm);
+    else if (g.nslot == 32) launch_direct_t<32, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, mirror, mode, st, tm);
+    else launch_direct_t<64, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, mirror, mode, st, tm);
 }
 
 template <bool OFF32>
@@ -1282,7 +1299,7 @@ static void launch_subsweep_n(const DevGeom& g, float* disk, const int16_t* n, i
 }
 
 hipError_t launch_subsweep_boundary(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
-                                    uint32_t sweep, unsigned long long* stats, int zl_begin, int zl_end,
+                                    uint32_t sweep, unsigned long long* stats, int* ovf, int zl_begin, int zl_end,
                                     float* mirror, int mirror_mode, hipStream_t st, const LaunchTiming* tm) {
     auto ceil_half = [](int v) { return v <= 0 ? 0 : (v + 1) / 2; };
     const int nczc = g.nz_local / 2;
@@ -1290,8 +1307,8 @@ hipError_t launch_subsweep_boundary(const DevGeom& g, float* disk, const int16_t
     if (cz1 > nczc) cz1 = nczc;
     if (cz1 <= cz0) return hipSuccess;
     const int64_t bytes = (int64_t)g.cps_x * g.cps_y * (g.nz_local + 2 * g.halo) * 3 * g.nmax * 4;
-    if (bytes < ((int64_t)1 << 32)) launch_direct_n<true>(g, disk, n, ox, oy, oz, sweep, stats, cz0, cz1 - cz0, mirror, mirror_mode, st, tm);
-    else launch_direct_n<false>(g, disk, n, ox, oy, oz, sweep, stats, cz0, cz1 - cz0, mirror, mirror_mode, st, tm);
+    if (bytes < ((int64_t)1 << 32)) launch_direct_n<true>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, cz1 - cz0, mirror, mirror_mode, st, tm);
+    else launch_direct_n<false>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, cz1 - cz0, mirror, mirror_mode, st, tm);
     return hipGetLastError();
 }
 
