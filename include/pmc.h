@@ -130,6 +130,15 @@ int pmc_sweep(pmc_ctx* ctx, uint32_t sweep);
  * context state (any mode; the slab driver interleaves these with halo exchange). */
 int pmc_phase(pmc_ctx* ctx, int colour, uint32_t sweep);
 int pmc_shift(pmc_ctx* ctx, uint32_t sweep);
+/* Slab contexts (halo = 1) after the 8 phases of a sweep, when both halo planes are exact copies
+ * of the neighbours' boundary planes: the sweep plan's shiftCells over the owned planes AND every
+ * halo plane whose new content depends only on planes this rank holds (along x/y both halos, along
+ * z in direction dir the one on the -dir side; shiftCells.h:46-108 applied to the halo copies, the
+ * same float operations as the plane's owner), then the buffer swap.  *halo_recv tells the caller
+ * which halo still has to be received: 0 none, +1 the top halo (local plane nz_local) from the rank
+ * above's new plane 0, -1 the bottom halo (plane -1) from the rank below's new top plane.  The C
+ * slab driver (pmc_slab_sweep) does the same internally. */
+int pmc_shift_slab(pmc_ctx* ctx, uint32_t sweep, int* halo_recv);
 /* Restrict a colour phase to the cells in local planes [zl_begin, zl_end) (0 <= .. <= nz_local).
  * Cells of one colour are independent, so splitting a phase into ranges in any order gives the
  * same result; the slab driver runs the halo-free interior while boundary planes travel. */

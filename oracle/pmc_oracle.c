@@ -341,13 +341,21 @@ void orc_subsweep_range(const pmc_params* p, float* disk, const int16_t* n, int 
 /* ------------------------------------------------------------------------------------- */
 int orc_shift_cells(const pmc_params* p, const float* din, const int16_t* nin, float* dout,
                     int16_t* nout, int f, float d) {
+    return orc_shift_cells_planes(p, din, nin, dout, nout, f, d, 0, p->nz_local);
+}
+
+/* The same over local planes [zl_begin, zl_end); a slab's halo planes (-1, nz_local) take the
+ * periodic global index of the plane they copy (the slab driver shifts the halo planes it can
+ * compute from its own data, pmc_shift_slab). */
+int orc_shift_cells_planes(const pmc_params* p, const float* din, const int16_t* nin, float* dout,
+                           int16_t* nout, int f, float d, int zl_begin, int zl_end) {
     const int nm = p->nmax;
     const float w = p->w;
     const int cps[3] = {p->cps_x, p->cps_y, p->cps_z};
     const float Lf = (float)cps[f] * w;
     const int dir = (d <= 0) ? -1 : 1;               /* shiftCells.h:46-53 */
     const float s = w * (float)dir;                  /* float s (fixed copy :28,84) */
-    const int64_t total = (int64_t)p->cps_x * p->cps_y * p->nz_local;
+    const int64_t total = (int64_t)p->cps_x * p->cps_y * (zl_end - zl_begin);
     int over = 0;
 #ifdef _OPENMP
 #pragma omp parallel for num_threads(g_threads > 0 ? g_threads : 1) if (g_threads > 0) \
@@ -355,8 +363,9 @@ int orc_shift_cells(const pmc_params* p, const float* din, const int16_t* nin, f
 #endif
     for (int64_t t = 0; t < total; ++t) {
         int x = (int)(t % p->cps_x), y = (int)((t / p->cps_x) % p->cps_y);
-        int zl = (int)(t / ((int64_t)p->cps_x * p->cps_y));
+        int zl = zl_begin + (int)(t / ((int64_t)p->cps_x * p->cps_y));
         int cid[3] = {x, y, p->z0 + zl};
+        if (cid[2] < 0) cid[2] += p->cps_z; else if (cid[2] >= p->cps_z) cid[2] -= p->cps_z;
         int64_t c = sidx(p, x, y, zl);
         float offset = (float)cid[f] * w - Lf / 2.0f;   /* :55 */
         /* neighbour in direction of f (:82-96) */

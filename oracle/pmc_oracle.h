@@ -42,6 +42,8 @@ void orc_subsweep_range(const pmc_params* p, float* disk, const int16_t* n, int 
 /* shiftCells (CUDA-Parallel-MC/CUDA-Parallel-MC/shiftCells.h:23-112) -- returns overflow count */
 int orc_shift_cells(const pmc_params* p, const float* din, const int16_t* nin, float* dout,
                     int16_t* nout, int f, float d);
+int orc_shift_cells_planes(const pmc_params* p, const float* din, const int16_t* nin, float* dout,
+                           int16_t* nout, int f, float d, int zl_begin, int zl_end);
 /* calc_energy (kernel.cu:452-470) as a cell-list sum over owned cells */
 double orc_energy(const pmc_params* p, const float* disk, const int16_t* n);
 /* whole-box driver loop (start.cu:237-260): nsweeps sweeps from `first`; state ends in

@@ -76,6 +76,7 @@ def lib():
                                          C.c_int, C.POINTER(Stats)]
         L.orc_subsweep_range.restype = None
         L.orc_shift_cells.argtypes = [P, _f32p, _i16p, _f32p, _i16p, C.c_int, C.c_float]
+        L.orc_shift_cells_planes.argtypes = [P, _f32p, _i16p, _f32p, _i16p, C.c_int, C.c_float, C.c_int, C.c_int]
         L.orc_energy.argtypes = [P, _f32p, _i16p]
         L.orc_energy.restype = C.c_double
         L.orc_run.argtypes = [P, _f32p, _i16p, _f32p, _i16p, C.c_uint32, C.c_int, C.POINTER(Stats)]

@@ -180,6 +180,21 @@ int enqueue_sweep(pmc_ctx* c, uint32_t sweep) {
     return PMC_OK;
 }
 
+// The planes a slab context's shiftCells covers after the 8 phases (local [*zl0, *zl1), halo
+// planes included) and which halo is left to receive (0 none, +1 top, -1 bottom): shiftCells
+// moves particles between a plane and its neighbour in direction dir along f, so along x/y every
+// halo plane is computable from the halo copy itself, along z the halo on the -dir side takes
+// particles from the owned plane next to it and the other needs the neighbour's new plane.
+int slab_shift_planes(int nz, const pmc_sweep_plan_t& plan, int* zl0, int* zl1) {
+    const int dir = plan.d <= 0.0f ? -1 : 1;   // k_shift / shiftCells.h:46-53
+    *zl0 = -1;
+    *zl1 = nz + 1;
+    if (plan.f != 2) return 0;
+    if (dir > 0) *zl1 = nz;
+    else *zl0 = 0;
+    return dir;
+}
+
 }  // namespace
 
 extern "C" {
@@ -434,6 +449,20 @@ int pmc_shift(pmc_ctx* c, uint32_t sweep) {
     int rc = pmc_shift_cells(c, c->disk[c->cur], c->n[c->cur], c->disk[c->cur ^ 1], c->n[c->cur ^ 1], plan.f,
                              plan.d);
     if (rc) return rc;
+    c->cur ^= 1;
+    return PMC_OK;
+}
+
+int pmc_shift_slab(pmc_ctx* c, uint32_t sweep, int* halo_recv) {
+    if (!c || !halo_recv) return fail(PMC_ERR_ARG, "null argument");
+    if (!c->P.halo) return fail(PMC_ERR_ARG, "pmc_shift_slab needs a slab context (halo = 1)");
+    const pmc_sweep_plan_t plan = pmc_plan_for_sweep(c->P.seed, sweep, c->P.w);
+    int zl0, zl1;
+    *halo_recv = slab_shift_planes(c->P.nz_local, plan, &zl0, &zl1);
+    LaunchTiming lt;
+    hipError_t e = launch_shift_planes(c->G, c->disk[c->cur], c->n[c->cur], c->disk[c->cur ^ 1], c->n[c->cur ^ 1],
+                                       plan.f, plan.d, c->flags, zl0, zl1, c->stream, next_timing(c, 1, &lt));
+    if (e != hipSuccess) return hip_fail(e, "shift launch");
     c->cur ^= 1;
     return PMC_OK;
 }
@@ -1022,9 +1051,8 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
     // planes (no exchange at all); along z in direction dir, the halo on the -dir side (it takes
     // particles from the owned plane next to it), and the other one is received: one plane with
     // its counts, one direction, instead of both planes.
-    const int dir = plan.d <= 0.0f ? -1 : 1;   // k_shift / shiftCells.h:46-53
-    int zl0 = -1, zl1 = nz + 1;
-    if (plan.f == 2) (dir > 0 ? zl1 : zl0) = dir > 0 ? nz : 0;
+    int zl0, zl1;
+    const int dir = slab_shift_planes(nz, plan, &zl0, &zl1);
     LaunchTiming lts;
     e = launch_shift_planes(c->G, c->disk[c->cur], c->n[c->cur], c->disk[c->cur ^ 1], c->n[c->cur ^ 1], plan.f,
                             plan.d, c->flags, zl0, zl1, S, next_timing(c, 1, &lts));
@@ -1032,7 +1060,7 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
     c->cur ^= 1;
     // the next sweep's first boundary launch follows the shift on T ("I(-1)" wait); its first
     // interior reads no halo, so it overlaps the z exchange
-    if (plan.f == 2) {
+    if (dir != 0) {
         PMC_HIP(hipEventRecord(s->ev_i, S));
         PMC_HIP(hipStreamWaitEvent(T, s->ev_i, 0));
         if ((rc = slab_exchange_zplane(c, dir))) return rc;

@@ -117,6 +117,7 @@ def lib():
         _sig(L, "pmc_timing", i32, _vp, i32, _vp, _vp, _vp, _vp)
         _sig(L, "pmc_subsweep_range", i32, _vp, _vp, _vp, C.POINTER(C.c_int * 3), u32, i32, i32)
         _sig(L, "pmc_shift", i32, _vp, u32)
+        _sig(L, "pmc_shift_slab", i32, _vp, u32, _vp)
         _sig(L, "pmc_start", i32, _vp, u32, i32, C.POINTER(Result))
         _sig(L, "pmc_run_graph", i32, _vp, u32, i32)
         _sig(L, "pmc_sweep_plan", i32, C.c_uint64, u32, C.c_float, C.POINTER(C.c_int * 8), C.POINTER(C.c_int),

@@ -190,6 +190,13 @@ class PmcContext:
     def shift(self, s: int) -> None:
         check("pmc_shift", lib().pmc_shift(self._h, s))
 
+    def shift_slab(self, s: int) -> int:
+        """Slab shiftCells incl. the locally computable halo planes (pmc_shift_slab); returns the
+        halo still to receive: 0 none, +1 top (from above's plane 0), -1 bottom (below's top plane)."""
+        h = C.c_int(0)
+        check("pmc_shift_slab", lib().pmc_shift_slab(self._h, s, C.byref(h)))
+        return h.value
+
     def start(self, first: int, passes: int) -> dict:
         r = Result()
         check("pmc_start", lib().pmc_start(self._h, first, passes, C.byref(r)))

@@ -8,7 +8,9 @@ planes, and only the boundary plane of the phase's z-parity changes:
 
   * after a phase with oz = 0 the owned plane 0 changed  -> it becomes the top halo of rank r-1;
   * after a phase with oz = 1 the owned plane nz-1 changed -> the bottom halo of rank r+1;
-  * after shiftCells every plane (and the counts) may change -> both halos are refreshed.
+  * after shiftCells every plane (and the counts) may change: the halo planes computable from the
+    rank's own copies are shifted with the owned ones (along x/y both, along z the one on the -dir
+    side), the other z halo receives the neighbour's new plane (pmc_shift_slab, as the C driver).
 
 The sweep plan (colour order, f, d) is a pure function of (seed, sweep) that every rank derives
 itself, and the RNG counters use GLOBAL cell ids, so the result is bit-identical to the
@@ -250,6 +252,26 @@ class SlabSimulation:
     def exchange_full(self) -> None:
         self.exchange_after_shift()
 
+    def _shift_and_exchange(self, s: int, run, stream=None):
+        """shiftCells after the 8 phases, C-driver rule (pmc_shift_slab): the engine also shifts
+        the halo planes it can compute from its own copies, so along x/y nothing travels and along z
+        one plane (with counts) goes one way.  Engines without shift_slab refresh both halos.
+        Returns the pending exchange."""
+        if not hasattr(self.engine, "shift_slab"):
+            run("shift", lambda: self.engine.shift(s), *([stream] if stream is not None else []))
+            self.cur ^= 1
+            return self._exchange(True, True, with_n=True, wait=False)
+        box = {}
+        run("shift", lambda: box.__setitem__("recv", self.engine.shift_slab(s)),
+            *([stream] if stream is not None else []))
+        self.cur ^= 1
+        recv = box["recv"]
+        if recv == 0:
+            return None
+        # +1: my top halo <- plane 0 of the rank above (each rank sends plane 0 down);
+        # -1: my bottom halo <- top plane of the rank below (each rank sends plane nz-1 up)
+        return self._exchange(send_down=recv > 0, send_up=recv < 0, with_n=True, wait=False)
+
     # ---- driver (start.cu:237-260 per slab) -------------------------------------------------
     def phase_only(self, colour: int, sweep: int) -> None:
         self.engine.phase(colour, sweep)
@@ -308,9 +330,7 @@ class SlabSimulation:
         S.wait_event(ev_i)
         S.wait_event(ev_b)
         self._wait(pending)
-        run("shift", lambda: self.engine.shift(s), S)
-        self.cur ^= 1
-        self._pending = self._exchange(True, True, with_n=True, wait=False)
+        self._pending = self._shift_and_exchange(s, run, S)
 
     def _sweep_one_stream(self, s: int, timer=None) -> None:
         """One sweep with communication hidden behind the halo-free interior.
@@ -336,9 +356,7 @@ class SlabSimulation:
             pending = self._exchange(send_down=(oz == 0), send_up=(oz == 1), with_n=False, wait=False,
                                      colour=colour)
         self._wait(pending)
-        run("shift", lambda: self.engine.shift(s))
-        self.cur ^= 1
-        self._pending = self._exchange(True, True, with_n=True, wait=False)
+        self._pending = self._shift_and_exchange(s, run)
 
     def finish(self) -> None:
         """Complete the outstanding halo exchange (call before reading the halos or the state)."""

@@ -36,6 +36,19 @@ class OracleEngine:
         assert over == 0
         self.cur ^= 1
 
+    def shift_slab(self, sweep):
+        """pmc_shift_slab's rule on the oracle: owned planes plus the locally computable halo
+        planes; returns the halo still to receive (0, +1 top, -1 bottom)."""
+        _, f, d = pmc_oracle.sweep_plan(self.p.seed, sweep, self.p.w)
+        nz = self.p.nz_local
+        recv = 0 if f != 2 else (1 if d > 0 else -1)
+        zl0, zl1 = (-1 if recv >= 0 else 0), (nz + 1 if recv <= 0 else nz)
+        over = pmc_oracle.lib().orc_shift_cells_planes(C.byref(self.p), self.d[self.cur], self.nn[self.cur],
+                                                       self.d[1 - self.cur], self.nn[1 - self.cur], f, d, zl0, zl1)
+        assert over == 0
+        self.cur ^= 1
+        return recv
+
 
     # restart hooks (the HIP engine's are PmcContext.save_snapshot / load_snapshot)
     def _owned(self):
@@ -88,7 +101,7 @@ def whole_box_from_slabs(cps, nz, world, nmax, owned_disks, owned_ns):
     return st
 
 
-def worker(rank, world, port, cps, nz, nmax, atoms, sweeps, out_q):
+def worker(rank, world, port, cps, nz, nmax, atoms, sweeps, out_q, first=0):
     import os
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -98,7 +111,7 @@ def worker(rank, world, port, cps, nz, nmax, atoms, sweeps, out_q):
         sim = make_oracle_slab(cps, nz, rank, world, nmax, atoms, TorchP2P(rank, world))
         d0, n0 = sim.owned()
         init = (d0.numpy().copy(), n0.numpy().copy())
-        sim.run(0, sweeps)
+        sim.run(first, sweeps)
         d1, n1 = sim.owned()
         out_q.put((rank, init, (d1.numpy().copy(), n1.numpy().copy()), sim.engine.stats.as_dict()))
     finally:

@@ -18,13 +18,15 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world,nz", [(2, 4), (2, 8), (3, 4)])
-def test_slab_ranks_equal_whole_box(oracle, world, nz):
-    cps, nmax, atoms, sweeps = 8, 16, 1000, 4
+# sweeps 0-3 shift along x/y only; 10-17 include z shifts in both directions (13-17), where each
+# rank shifts one halo plane itself and receives the other from its neighbour
+@pytest.mark.parametrize("world,nz,first,sweeps", [(2, 4, 0, 4), (2, 8, 10, 8), (3, 4, 10, 8), (4, 4, 12, 6)])
+def test_slab_ranks_equal_whole_box(oracle, world, nz, first, sweeps):
+    cps, nmax, atoms = 8, 16, 1000
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=slab_helpers.worker, args=(r, world, port, cps, nz, nmax, atoms, sweeps, q))
+    procs = [ctx.Process(target=slab_helpers.worker, args=(r, world, port, cps, nz, nmax, atoms, sweeps, q, first))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -39,7 +41,7 @@ def test_slab_ranks_equal_whole_box(oracle, world, nz):
     st = slab_helpers.whole_box_from_slabs(cps, nz, world, nmax, [res[r][0][0] for r in range(world)],
                                            [res[r][0][1] for r in range(world)])
     assert int(st.n.sum()) == atoms * world
-    assert st.run(0, sweeps) == 0
+    assert st.run(first, sweeps) == 0
     got_d = np.concatenate([res[r][1][0].reshape(-1) for r in range(world)])
     got_n = np.concatenate([res[r][1][1].reshape(-1) for r in range(world)])
     assert np.array_equal(got_n, st.n)
