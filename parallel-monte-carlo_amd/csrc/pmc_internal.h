@@ -10,10 +10,13 @@
 namespace pmc {
 
 constexpr int kWave = 64;          // CDNA wavefront
+// Waves per subsweep workgroup.  One: each wave is its own workgroup (5 KiB of LDS), so a CU
+// refills a retiring wave's slot at once instead of when all waves of its workgroup are done;
+// measured 2% faster per phase than 4 (and 6% faster than 8) at 128^3 / 1e7 (tools/bench_ab.sh).
 #ifndef PMC_SUBWAVES
-#define PMC_SUBWAVES 4
+#define PMC_SUBWAVES 1
 #endif
-constexpr int kSubWaves = PMC_SUBWAVES;   // cells (waves) per subsweep workgroup
+constexpr int kSubWaves = PMC_SUBWAVES;
 constexpr int kStatSlots = 1024;   // stats accumulator slots per counter (contention spread)
 // subsweep LDS per wave for a partner capacity lcap: x, y, z rows of `stride` slots
 // (stride = lcap rounded up to 64 with >= 32 slots of tail: the tail is the discard target of the
