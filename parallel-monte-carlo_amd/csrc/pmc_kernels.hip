@@ -919,8 +919,13 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_fallback(DevGeom
 // shiftCells: NSLOT lanes per cell, ballot compaction (shiftCells.h:28-144; float s of the fixed
 // copy CUDA-Parallel-MC/CUDA-Parallel-MC/shiftCells.h:23-112).  Double-buffered.
 // ------------------------------------------------------------------------------------------
+#ifndef PMC_SHIFT_THREADS
+#define PMC_SHIFT_THREADS 256   // k_shift workgroup size
+#endif
+constexpr int kShiftThreads = PMC_SHIFT_THREADS;
+
 template <int NSLOT, int U>
-__global__ __launch_bounds__(256) void k_shift(DevGeom g, const float* __restrict__ din,
+__global__ __launch_bounds__(kShiftThreads) void k_shift(DevGeom g, const float* __restrict__ din,
                                                const int16_t* __restrict__ nin, float* __restrict__ dout,
                                                int16_t* __restrict__ nout, int f, float d,
                                                uint32_t* __restrict__ flags, int zl0) {
@@ -929,7 +934,7 @@ __global__ __launch_bounds__(256) void k_shift(DevGeom g, const float* __restric
     // from its own data instead of receiving them).  NSLOT lanes per cell, CPB cells per block
     // along x per unrolled step j, U steps whose loads are all issued before any use (U times
     // the bytes in flight per wave: the kernel is latency-bound at one cell per lane group)
-    constexpr int CPB = 256 / NSLOT;
+    constexpr int CPB = kShiftThreads / NSLOT;
     const int lane = threadIdx.x & (kWave - 1);
     const int p = threadIdx.x & (NSLOT - 1);
     const int y = (int)blockIdx.y, zl = zl0 + (int)blockIdx.z;
@@ -1344,8 +1349,9 @@ hipError_t launch_shift_planes(const DevGeom& g, const float* din, const int16_t
 #define PMC_SHIFT_U 8
 #endif
     constexpr int U = PMC_SHIFT_U;   // cells per lane group, loads hoisted
-    const int cpb = 256 / g.nslot;
-    dim3 grid((unsigned)((g.cps_x + cpb * U - 1) / (cpb * U)), (unsigned)g.cps_y, (unsigned)(zl_end - zl_begin)), block(256);
+    const int cpb = kShiftThreads / g.nslot;
+    dim3 grid((unsigned)((g.cps_x + cpb * U - 1) / (cpb * U)), (unsigned)g.cps_y, (unsigned)(zl_end - zl_begin)),
+        block(kShiftThreads);
     const int z0 = zl_begin;
     switch (g.nslot) {
         case 8: launch_k(k_shift<8, U>, grid, block, 0, st, tm, g, din, nin, dout, nout, f, d, flags, z0); break;
