@@ -838,7 +838,9 @@ __global__ __launch_bounds__(kWave * kSubWaves) __attribute__((amdgpu_waves_per_
     // XCD-aware block order: blocks b and b+8 share an XCD (round-robin dispatch), so give each
     // XCD a contiguous run of cells -> neighbouring stencils share that XCD's L2.  Speed only.
     uint32_t nblk = gridDim.x, b = blockIdx.x;
+#ifndef PMC_NO_XCD_REMAP
     if ((nblk & 7u) == 0u) b = (b & 7u) * (nblk >> 3) + (b >> 3);
+#endif
     const int total = (g.cps_x >> 1) * (g.cps_y >> 1) * ncz;
 #if PMC_CELLS_PER_WAVE == 2
     // two cells per wave (shared stencil table and RNG pass): wave w takes cells 2w and 2w+1
