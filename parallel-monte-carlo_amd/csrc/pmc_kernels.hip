@@ -675,7 +675,11 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
     }
     // fixed-point conversion only when something was accepted (pmc_to_fixed(0) == 0)
     const int64_t de_fix = n_acc ? pmc_to_fixed(de_cell) : 0;
+#ifdef PMC_PROBE_NO_STATS   // timing probe only (the counters stay zero): cost of the stats atomics
+    if (lane == 0 && de_fix == 0x7fffffffffffffffll) {
+#else
     if (lane == 0) {
+#endif
         const int slot = t & (kStatSlots - 1);
         atomicAdd(&stats[0 * kStatSlots + slot], (unsigned long long)de_fix);
         atomicAdd(&stats[1 * kStatSlots + slot], (unsigned long long)n_acc);
