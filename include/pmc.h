@@ -166,6 +166,19 @@ int pmc_comm_unique_id(unsigned char id[128]);
  * rank 0), the auxiliary stream and the halo buffers.  id = NULL with world = 1: no RCCL, the
  * periodic halos are local copies. */
 int pmc_slab_init(pmc_ctx* ctx, int rank, int world, const unsigned char* id);
+/* In-process halo transport: `world` slab contexts of ONE process (e.g. W slabs on one GPU), one
+ * host thread per rank.  The slab driver issues exactly the messages it gives RCCL (same peers,
+ * same order, same ncclSend/ncclRecv matching); each becomes a device-to-device copy on the
+ * receiver's aux stream, ordered by HIP events and a host barrier per exchange.  Every rank must
+ * call the collective functions (pmc_slab_exchange, pmc_slab_sweep) from its own thread.  A rank
+ * that fails, or a barrier that waits longer than PMC_LOCAL_GROUP_TIMEOUT_MS (default 120000),
+ * breaks the group: every later exchange returns PMC_ERR_HIP.  Destroy the contexts before the
+ * group. */
+typedef struct pmc_local_group pmc_local_group;
+int pmc_local_group_create(int world, pmc_local_group** out);
+void pmc_local_group_destroy(pmc_local_group* group);
+/* pmc_slab_init with the in-process transport: rank `rank` of group->world. */
+int pmc_slab_init_local(pmc_ctx* ctx, int rank, pmc_local_group* group);
 /* Refill both halo planes and their counts from the neighbours (after init_lattice, copy_in or
  * load_snapshot).  Collective. */
 int pmc_slab_exchange(pmc_ctx* ctx);

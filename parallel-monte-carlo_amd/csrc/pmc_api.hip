@@ -5,8 +5,11 @@
 // is asynchronous on the context stream; only the *_read / copy / synchronize calls block.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
+#include <mutex>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -795,15 +798,83 @@ int nccl_fail(ncclResult_t e, const char* what) {
 
 }  // namespace
 
+// ---- halo transports --------------------------------------------------------------------------
+// Every halo exchange of the slab driver is a list of point-to-point messages (sends and receives
+// of byte ranges, with ncclSend/ncclRecv matching: the k-th send from rank a to rank b fills the
+// k-th receive on b from a) issued on the aux stream.  Two transports carry them:
+//   * RCCL (one process per GPU, the product multi-GPU path): one ncclGroupStart/End per list;
+//   * an in-process group (pmc_local_group): W slab contexts of ONE process, one host thread per
+//     rank, device-to-device copies ordered by HIP events and a host barrier -- the same schedule,
+//     peers and message lists as RCCL, so W ranks run on one GPU ("a local-copy halo
+//     transport behind the same interface as the RCCL transport").
+// A single rank without either keeps its periodic halos by local copies (no messages at all).
+struct XferMsg {
+    void* buf;
+    size_t bytes;
+    int peer;
+};
+
+struct pmc_local_group {
+    struct Slot {
+        hipEvent_t ready = nullptr;    // the rank's aux stream after its send buffers were written
+        hipEvent_t pulled = nullptr;   // ... after its receives (copies from the peers' buffers)
+        std::vector<XferMsg> sends, recvs;
+        bool joined = false;
+    };
+    int world = 0;
+    int timeout_ms = 120000;
+    std::mutex m;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t generation = 0;
+    bool broken = false;
+    std::vector<Slot> slot;
+};
+
+namespace {
+
+// host barrier of the in-process group; PMC_ERR_HIP when a rank failed or the wait timed out (a
+// rank that never arrives must not hang the others: the group is marked broken)
+int group_barrier(pmc_local_group* g) {
+    std::unique_lock<std::mutex> lk(g->m);
+    if (g->broken) return fail(PMC_ERR_HIP, "local group: another rank failed");
+    const uint64_t gen = g->generation;
+    if (++g->arrived == g->world) {
+        g->arrived = 0;
+        ++g->generation;
+        g->cv.notify_all();
+        return PMC_OK;
+    }
+    const bool ok = g->cv.wait_for(lk, std::chrono::milliseconds(g->timeout_ms),
+                                   [&] { return g->generation != gen || g->broken; });
+    if (!ok || g->broken) {
+        g->broken = true;
+        g->cv.notify_all();
+        return fail(PMC_ERR_HIP, ok ? "local group: another rank failed" : "local group: barrier timed out");
+    }
+    return PMC_OK;
+}
+
+void group_break(pmc_local_group* g) {
+    std::lock_guard<std::mutex> lk(g->m);
+    g->broken = true;
+    g->cv.notify_all();
+}
+
+}  // namespace
+
 struct pmc_slab {
     int rank = 0, world = 1, below = 0, above = 0;
-    ncclComm_t comm = nullptr;            // null: one rank, halos by local copies
+    ncclComm_t comm = nullptr;            // RCCL transport
+    pmc_local_group* group = nullptr;     // in-process transport (not owned)
     hipStream_t aux = nullptr;            // boundary planes + exchanges ("T")
     hipEvent_t ev_i = nullptr, ev_b = nullptr, ev_t = nullptr;
     float* sbuf = nullptr;                // packed colour cells of the sent plane
     float* rbuf = nullptr;                // ... of the received plane
     size_t pack_floats = 0;
     int pend_colour = -1, pend_dst = 0;   // unpack owed on aux (colour, halo plane)
+    std::vector<XferMsg> sends, recvs;    // the exchange being assembled
+    bool messages() const { return comm != nullptr || group != nullptr; }
 };
 
 namespace {
@@ -813,6 +884,10 @@ void drop_slab(pmc_ctx* c) {
     if (!s) return;
     if (s->aux) (void)hipStreamSynchronize(s->aux);
     if (s->comm && rccl().ok) (void)rccl().comm_destroy(s->comm);
+    if (s->group) {
+        std::lock_guard<std::mutex> lk(s->group->m);
+        s->group->slot[s->rank].joined = false;
+    }
     if (s->aux) (void)hipStreamDestroy(s->aux);
     for (hipEvent_t e : {s->ev_i, s->ev_b, s->ev_t})
         if (e) (void)hipEventDestroy(e);
@@ -820,6 +895,86 @@ void drop_slab(pmc_ctx* c) {
     if (s->rbuf) (void)hipFree(s->rbuf);
     delete s;
     c->slab = nullptr;
+}
+
+// queue one message of the current exchange
+void xfer_send(pmc_slab* s, const void* buf, size_t bytes, int peer) {
+    s->sends.push_back({const_cast<void*>(buf), bytes, peer});
+}
+void xfer_recv(pmc_slab* s, void* buf, size_t bytes, int peer) { s->recvs.push_back({buf, bytes, peer}); }
+
+// carry the queued messages on the aux stream (RCCL group, or the in-process group's copies)
+int xfer_run(pmc_slab* s) {
+    std::vector<XferMsg> sends, recvs;
+    sends.swap(s->sends);
+    recvs.swap(s->recvs);
+    if (s->comm) {
+        Rccl& R = rccl();
+        PMC_NCCL(R.group_start());
+        for (const XferMsg& m : sends) PMC_NCCL(R.send(m.buf, m.bytes, ncclUint8, m.peer, s->comm, s->aux));
+        for (const XferMsg& m : recvs) PMC_NCCL(R.recv(m.buf, m.bytes, ncclUint8, m.peer, s->comm, s->aux));
+        PMC_NCCL(R.group_end());
+        return PMC_OK;
+    }
+    pmc_local_group* g = s->group;
+    if (!g) return fail(PMC_ERR_ARG, "slab exchange without a transport");
+    pmc_local_group::Slot& me = g->slot[s->rank];
+    // 1. publish the send list and an event after the work that wrote the send buffers
+    hipError_t e = hipEventRecord(me.ready, s->aux);
+    if (e != hipSuccess) { group_break(g); return hip_fail(e, "hipEventRecord"); }
+    {
+        std::lock_guard<std::mutex> lk(g->m);
+        me.sends = sends;
+        me.recvs = recvs;
+    }
+    int rc = group_barrier(g);
+    if (rc) return rc;
+    // 2. pull: the k-th receive from peer p copies p's k-th send to this rank (RCCL matching)
+    std::vector<int> taken(g->world, 0);
+    for (const XferMsg& m : recvs) {
+        const pmc_local_group::Slot& src = g->slot[m.peer];
+        const XferMsg* hit = nullptr;
+        int k = 0;
+        for (const XferMsg& sm : src.sends)
+            if (sm.peer == s->rank && k++ == taken[m.peer]) { hit = &sm; break; }
+        if (!hit || hit->bytes != m.bytes) {
+            group_break(g);
+            return fail(PMC_ERR_ARG, "local group: unmatched or mis-sized halo message");
+        }
+        ++taken[m.peer];
+        if ((e = hipStreamWaitEvent(s->aux, src.ready, 0)) != hipSuccess ||
+            (e = hipMemcpyAsync(m.buf, hit->buf, m.bytes, hipMemcpyDeviceToDevice, s->aux)) != hipSuccess) {
+            group_break(g);
+            return hip_fail(e, "local group: halo copy");
+        }
+    }
+    if ((e = hipEventRecord(me.pulled, s->aux)) != hipSuccess) { group_break(g); return hip_fail(e, "hipEventRecord"); }
+    // every send must be received (the slots are stable between the two barriers: a rank publishes
+    // its next lists only after the second one)
+    std::vector<char> readers(g->world, 0);
+    for (const XferMsg& m : sends) {
+        if (readers[m.peer]) continue;
+        readers[m.peer] = 1;
+        int want = 0, got = 0;
+        for (const XferMsg& x : sends) want += x.peer == m.peer;
+        for (const XferMsg& x : g->slot[m.peer].recvs) got += x.peer == s->rank;
+        if (want != got) {
+            group_break(g);
+            return fail(PMC_ERR_ARG, "local group: a halo message was not received");
+        }
+    }
+    if ((rc = group_barrier(g))) return rc;
+    // 3. every peer that read this rank's buffers is done before the aux stream writes them again
+    //    (RCCL's send completes the same way); a peer re-records `pulled` only after the next
+    //    exchange's first barrier, which this rank has not reached yet
+    for (int p = 0; p < g->world; ++p) {
+        if (!readers[p]) continue;
+        if ((e = hipStreamWaitEvent(s->aux, g->slot[p].pulled, 0)) != hipSuccess) {
+            group_break(g);
+            return hip_fail(e, "hipStreamWaitEvent");
+        }
+    }
+    return PMC_OK;
 }
 
 size_t plane_floats(const pmc_ctx* c) { return (size_t)c->P.cps_x * c->P.cps_y * 3 * c->P.nmax; }
@@ -845,14 +1000,13 @@ int slab_complete(pmc_ctx* c) {
 // A single rank needs nothing here: its boundary launch mirrored the rows into its own halo.
 int slab_exchange_phase(pmc_ctx* c, int colour) {
     pmc_slab* s = c->slab;
-    if (!s->comm) return PMC_OK;
+    if (!s->messages()) return PMC_OK;
     const bool down = colour % 2 == 0;                 // oz = 0: plane 0 -> below, top halo <- above
     const int to = down ? s->below : s->above, from = down ? s->above : s->below;
-    Rccl& R = rccl();
-    PMC_NCCL(R.group_start());
-    PMC_NCCL(R.send(s->sbuf, s->pack_floats, ncclFloat32, to, s->comm, s->aux));
-    PMC_NCCL(R.recv(s->rbuf, s->pack_floats, ncclFloat32, from, s->comm, s->aux));
-    PMC_NCCL(R.group_end());
+    xfer_send(s, s->sbuf, s->pack_floats * 4, to);
+    xfer_recv(s, s->rbuf, s->pack_floats * 4, from);
+    int rc = xfer_run(s);
+    if (rc) return rc;
     s->pend_colour = colour;
     s->pend_dst = down ? c->P.nz_local : -1;
     return PMC_OK;
@@ -863,7 +1017,7 @@ int slab_exchange_full(pmc_ctx* c) {
     pmc_slab* s = c->slab;
     const int nz = c->P.nz_local;
     const size_t pf = plane_floats(c), pc = plane_cells(c);
-    if (!s->comm) {
+    if (!s->messages()) {
         PMC_HIP(hipMemcpyAsync(disk_plane(c, nz), disk_plane(c, 0), pf * 4, hipMemcpyDeviceToDevice, s->aux));
         PMC_HIP(hipMemcpyAsync(n_plane(c, nz), n_plane(c, 0), pc * 2, hipMemcpyDeviceToDevice, s->aux));
         PMC_HIP(hipMemcpyAsync(disk_plane(c, -1), disk_plane(c, nz - 1), pf * 4, hipMemcpyDeviceToDevice, s->aux));
@@ -871,18 +1025,16 @@ int slab_exchange_full(pmc_ctx* c) {
         return PMC_OK;
     }
     // per peer, sends and receives match in issue order: (plane, counts) down, then up
-    Rccl& R = rccl();
-    PMC_NCCL(R.group_start());
-    PMC_NCCL(R.send(disk_plane(c, 0), pf, ncclFloat32, s->below, s->comm, s->aux));
-    PMC_NCCL(R.send(n_plane(c, 0), pc * 2, ncclUint8, s->below, s->comm, s->aux));
-    PMC_NCCL(R.send(disk_plane(c, nz - 1), pf, ncclFloat32, s->above, s->comm, s->aux));
-    PMC_NCCL(R.send(n_plane(c, nz - 1), pc * 2, ncclUint8, s->above, s->comm, s->aux));
-    PMC_NCCL(R.recv(disk_plane(c, nz), pf, ncclFloat32, s->above, s->comm, s->aux));
-    PMC_NCCL(R.recv(n_plane(c, nz), pc * 2, ncclUint8, s->above, s->comm, s->aux));
-    PMC_NCCL(R.recv(disk_plane(c, -1), pf, ncclFloat32, s->below, s->comm, s->aux));
-    PMC_NCCL(R.recv(n_plane(c, -1), pc * 2, ncclUint8, s->below, s->comm, s->aux));
-    PMC_NCCL(R.group_end());
-    return PMC_OK;
+    // (counts travel as bytes: RCCL has no 16-bit integer type)
+    xfer_send(s, disk_plane(c, 0), pf * 4, s->below);
+    xfer_send(s, n_plane(c, 0), pc * 2, s->below);
+    xfer_send(s, disk_plane(c, nz - 1), pf * 4, s->above);
+    xfer_send(s, n_plane(c, nz - 1), pc * 2, s->above);
+    xfer_recv(s, disk_plane(c, nz), pf * 4, s->above);
+    xfer_recv(s, n_plane(c, nz), pc * 2, s->above);
+    xfer_recv(s, disk_plane(c, -1), pf * 4, s->below);
+    xfer_recv(s, n_plane(c, -1), pc * 2, s->below);
+    return xfer_run(s);
 }
 
 // after a shift along z in direction dir: the halo on the +dir side takes the neighbour's new
@@ -892,20 +1044,17 @@ int slab_exchange_zplane(pmc_ctx* c, int dir) {
     const int nz = c->P.nz_local;
     const size_t pf = plane_floats(c), pc = plane_cells(c);
     const int src = dir > 0 ? 0 : nz - 1, dst = dir > 0 ? nz : -1;   // my plane -> the -dir rank's halo
-    if (!s->comm) {
+    if (!s->messages()) {
         PMC_HIP(hipMemcpyAsync(disk_plane(c, dst), disk_plane(c, src), pf * 4, hipMemcpyDeviceToDevice, s->aux));
         PMC_HIP(hipMemcpyAsync(n_plane(c, dst), n_plane(c, src), pc * 2, hipMemcpyDeviceToDevice, s->aux));
         return PMC_OK;
     }
     const int to = dir > 0 ? s->below : s->above, from = dir > 0 ? s->above : s->below;
-    Rccl& R = rccl();
-    PMC_NCCL(R.group_start());
-    PMC_NCCL(R.send(disk_plane(c, src), pf, ncclFloat32, to, s->comm, s->aux));
-    PMC_NCCL(R.send(n_plane(c, src), pc * 2, ncclUint8, to, s->comm, s->aux));
-    PMC_NCCL(R.recv(disk_plane(c, dst), pf, ncclFloat32, from, s->comm, s->aux));
-    PMC_NCCL(R.recv(n_plane(c, dst), pc * 2, ncclUint8, from, s->comm, s->aux));
-    PMC_NCCL(R.group_end());
-    return PMC_OK;
+    xfer_send(s, disk_plane(c, src), pf * 4, to);
+    xfer_send(s, n_plane(c, src), pc * 2, to);
+    xfer_recv(s, disk_plane(c, dst), pf * 4, from);
+    xfer_recv(s, n_plane(c, dst), pc * 2, from);
+    return xfer_run(s);
 }
 
 }  // namespace
@@ -923,12 +1072,16 @@ int pmc_comm_unique_id(unsigned char id[128]) {
     return PMC_OK;
 }
 
-int pmc_slab_init(pmc_ctx* c, int rank, int world, const unsigned char* id) {
+}  // extern "C"
+
+namespace {
+
+// common part of pmc_slab_init / pmc_slab_init_local: streams, events, overflow queue, buffers
+int slab_attach(pmc_ctx* c, int rank, int world, bool messages) {
     if (!c || world < 1 || rank < 0 || rank >= world) return fail(PMC_ERR_ARG, "bad argument");
     if (c->P.halo != 1) return fail(PMC_ERR_ARG, "pmc_slab_init needs a slab context (halo = 1)");
     if (c->P.nz_local < 2 || c->P.z0 != rank * c->P.nz_local || c->P.cps_z != world * c->P.nz_local)
         return fail(PMC_ERR_ARG, "slab geometry must be z0 = rank*nz_local, cps_z = world*nz_local");
-    if (!id && world != 1) return fail(PMC_ERR_ARG, "more than one rank needs an RCCL unique id");
     PMC_HIP(hipStreamSynchronize(c->stream));
     drop_slab(c);
     pmc_slab* s = new pmc_slab();
@@ -954,27 +1107,78 @@ int pmc_slab_init(pmc_ctx* c, int rank, int world, const unsigned char* id) {
             return hip_fail(e, "hipMalloc overflow queue");
         }
     }
-    if (id) {
-        Rccl& R = rccl();
-        if (!R.ok) {
-            drop_slab(c);
-            return fail(PMC_ERR_HIP, R.err);
-        }
+    if (messages) {
         if ((e = hipMalloc(&s->sbuf, s->pack_floats * 4)) != hipSuccess ||
             (e = hipMalloc(&s->rbuf, s->pack_floats * 4)) != hipSuccess) {
             drop_slab(c);
             return hip_fail(e, "hipMalloc halo buffers");
         }
-        ncclUniqueId u;
-        std::memcpy(&u, id, 128);
-        ncclResult_t r = R.comm_init_rank(&s->comm, world, u, rank);
-        if (r != ncclSuccess) {
-            s->comm = nullptr;
-            int rc = nccl_fail(r, "ncclCommInitRank");
-            drop_slab(c);
-            return rc;
+    }
+    return PMC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pmc_slab_init(pmc_ctx* c, int rank, int world, const unsigned char* id) {
+    if (!id && world != 1) return fail(PMC_ERR_ARG, "more than one rank needs an RCCL unique id");
+    if (id && !rccl().ok) return fail(PMC_ERR_HIP, rccl().err);
+    int rc = slab_attach(c, rank, world, id != nullptr);
+    if (rc || !id) return rc;
+    pmc_slab* s = c->slab;
+    ncclUniqueId u;
+    std::memcpy(&u, id, 128);
+    ncclResult_t r = rccl().comm_init_rank(&s->comm, world, u, rank);
+    if (r != ncclSuccess) {
+        s->comm = nullptr;
+        rc = nccl_fail(r, "ncclCommInitRank");
+        drop_slab(c);
+        return rc;
+    }
+    return PMC_OK;
+}
+
+int pmc_local_group_create(int world, pmc_local_group** out) {
+    if (!out || world < 1) return fail(PMC_ERR_ARG, "bad argument");
+    *out = nullptr;
+    pmc_local_group* g = new pmc_local_group();
+    g->world = world;
+    g->slot.resize((size_t)world);
+    for (auto& sl : g->slot) {
+        hipError_t e;
+        if ((e = hipEventCreateWithFlags(&sl.ready, hipEventDisableTiming)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&sl.pulled, hipEventDisableTiming)) != hipSuccess) {
+            pmc_local_group_destroy(g);
+            return hip_fail(e, "hipEventCreate");
         }
     }
+    const char* t = std::getenv("PMC_LOCAL_GROUP_TIMEOUT_MS");
+    if (t && std::atoi(t) > 0) g->timeout_ms = std::atoi(t);
+    *out = g;
+    return PMC_OK;
+}
+
+void pmc_local_group_destroy(pmc_local_group* g) {
+    if (!g) return;
+    for (auto& sl : g->slot) {
+        if (sl.ready) (void)hipEventDestroy(sl.ready);
+        if (sl.pulled) (void)hipEventDestroy(sl.pulled);
+    }
+    delete g;
+}
+
+int pmc_slab_init_local(pmc_ctx* c, int rank, pmc_local_group* g) {
+    if (!c || !g || rank < 0 || rank >= g->world) return fail(PMC_ERR_ARG, "bad argument");
+    {
+        std::lock_guard<std::mutex> lk(g->m);
+        if (g->slot[rank].joined) return fail(PMC_ERR_ARG, "local group: rank already attached");
+    }
+    int rc = slab_attach(c, rank, g->world, true);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(g->m);
+    g->slot[rank].joined = true;
+    c->slab->group = g;
     return PMC_OK;
 }
 
@@ -1031,10 +1235,10 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
         // rows go straight to the send buffer (RCCL) or to the periodic halo (single rank)
         const bool down = o[2] == 0;
         const int zb = down ? 0 : nz - 1;
-        float* mirror = s->comm ? s->sbuf : disk_plane(c, down ? nz : -1);
+        float* mirror = s->messages() ? s->sbuf : disk_plane(c, down ? nz : -1);
         LaunchTiming lt;
         e = launch_subsweep_boundary(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep, c->stats, c->ovf_aux, zb,
-                                     zb + 1, mirror, s->comm ? 0 : 1, T, next_timing(c, 0, &lt));
+                                     zb + 1, mirror, s->messages() ? 0 : 1, T, next_timing(c, 0, &lt));
         if (e != hipSuccess) return hip_fail(e, "subsweep launch");
         PMC_HIP(hipEventRecord(s->ev_b, T));
         // exchange k and its unpack follow B(k) on T straight away, so they run beside I(k)

@@ -110,6 +110,9 @@ def lib():
         _sig(L, "pmc_phase_range_on", i32, _vp, i32, u32, i32, i32, _vp)
         _sig(L, "pmc_comm_unique_id", i32, _vp)
         _sig(L, "pmc_slab_init", i32, _vp, i32, i32, _vp)
+        _sig(L, "pmc_local_group_create", i32, i32, C.POINTER(_vp))
+        _sig(L, "pmc_local_group_destroy", None, _vp)
+        _sig(L, "pmc_slab_init_local", i32, _vp, i32, _vp)
         _sig(L, "pmc_slab_exchange", i32, _vp)
         _sig(L, "pmc_slab_sweep", i32, _vp, u32)
         _sig(L, "pmc_slab_finish", i32, _vp)

@@ -164,6 +164,10 @@ class PmcContext:
         uid = None if unique_id is None else (C.c_ubyte * 128).from_buffer_copy(unique_id)
         check("pmc_slab_init", lib().pmc_slab_init(self._h, rank, world, uid))
 
+    def slab_init_local(self, rank: int, group: "LocalGroup") -> None:
+        """pmc_slab_init with the in-process transport (W slabs of one process, a thread per rank)."""
+        check("pmc_slab_init_local", lib().pmc_slab_init_local(self._h, rank, group.handle))
+
     def slab_exchange(self) -> None:
         check("pmc_slab_exchange", lib().pmc_slab_exchange(self._h))
 
@@ -267,6 +271,22 @@ class PmcContext:
         check("pmc_plane_span", lib().pmc_plane_span(self._h, z_local, C.byref(a), C.byref(b), C.byref(c),
                                                      C.byref(d)))
         return a.value, b.value, c.value, d.value
+
+
+class LocalGroup:
+    """pmc_local_group: the in-process halo transport shared by `world` slab contexts of this
+    process.  Close (or drop) the contexts before the group."""
+
+    def __init__(self, world: int):
+        h = C.c_void_p()
+        check("pmc_local_group_create", lib().pmc_local_group_create(world, C.byref(h)))
+        self.handle = h
+        self.world = world
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib().pmc_local_group_destroy(self.handle)
+            self.handle = None
 
 
 def comm_unique_id() -> bytes:

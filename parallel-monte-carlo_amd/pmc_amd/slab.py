@@ -406,31 +406,42 @@ class SlabDriver:
 
     def __init__(self, cps: int, nz_local: int, rank: int, world: int, stream=None, atoms_per_rank: int = 0,
                  atoms_total: int = 0, nmax: int = 16, n_moves: int = 10, seed: int = 1234,
-                 use_rccl: Optional[bool] = None, group=None):
-        import torch
+                 use_rccl: Optional[bool] = None, group=None, local_group=None, cps_y: int = 0):
+        """local_group: a pmc_amd.engine.LocalGroup -- the in-process transport (this rank is one of
+        local_group.world slab contexts of this process; construct and drive each rank from its
+        own thread: the exchanges are collective)."""
         from .engine import PmcContext, comm_unique_id
         self.g = SlabGeometry(cps, nz_local, rank, world, nmax)
-        if stream is None:
+        if stream is None and local_group is None:
+            import torch
             stream = torch.cuda.Stream()
         self.stream = stream
-        self.ctx = PmcContext(cps, cps_z=self.g.cps_z, nz_local=nz_local, z0=self.g.z0, halo=1, nmax=nmax,
-                              n_moves=n_moves, seed=seed, stream=stream.cuda_stream)
-        use_rccl = world > 1 if use_rccl is None else use_rccl
-        uid = None
-        if use_rccl:
-            lib_path = _rccl_lib_path()
-            if lib_path and not os.environ.get("PMC_RCCL_LIB"):
-                os.environ["PMC_RCCL_LIB"] = lib_path
-            buf = torch.zeros(128, dtype=torch.uint8)
-            if rank == 0:
-                buf = torch.tensor(list(comm_unique_id()), dtype=torch.uint8)
-            if world > 1:
-                import torch.distributed as dist
-                on = buf.cuda() if dist.get_backend(group) == "nccl" else buf
-                dist.broadcast(on, src=0, group=group)
-                buf = on.cpu()
-            uid = bytes(buf.numpy().tobytes())
-        self.ctx.slab_init(rank, world, uid)      # RCCL communicator: collective over the ranks
+        self.ctx = PmcContext(cps, cps_y=cps_y, cps_z=self.g.cps_z, nz_local=nz_local, z0=self.g.z0, halo=1,
+                              nmax=nmax, n_moves=n_moves, seed=seed,
+                              stream=stream.cuda_stream if stream is not None else None)
+        self.cps_y = cps_y or cps
+        if local_group is not None:
+            if local_group.world != world:
+                raise ValueError("local_group.world != world")
+            self.ctx.slab_init_local(rank, local_group)
+        else:
+            use_rccl = world > 1 if use_rccl is None else use_rccl
+            uid = None
+            if use_rccl:
+                import torch
+                lib_path = _rccl_lib_path()
+                if lib_path and not os.environ.get("PMC_RCCL_LIB"):
+                    os.environ["PMC_RCCL_LIB"] = lib_path
+                buf = torch.zeros(128, dtype=torch.uint8)
+                if rank == 0:
+                    buf = torch.tensor(list(comm_unique_id()), dtype=torch.uint8)
+                if world > 1:
+                    import torch.distributed as dist
+                    on = buf.cuda() if dist.get_backend(group) == "nccl" else buf
+                    dist.broadcast(on, src=0, group=group)
+                    buf = on.cpu()
+                uid = bytes(buf.numpy().tobytes())
+            self.ctx.slab_init(rank, world, uid)      # RCCL communicator: collective over the ranks
         if atoms_total:
             self.ctx.init_lattice_global(atoms_total)
             self.ctx.slab_exchange()
@@ -454,7 +465,7 @@ class SlabDriver:
         halos refilled from the neighbours."""
         import numpy as np
         full_d, full_n = self.ctx.copy_out()
-        plane = self.g.cps * self.g.cps
+        plane = self.g.cps * self.cps_y
         row = 3 * self.g.nmax
         full_d[plane * row:(self.g.nz + 1) * plane * row] = np.asarray(disk, np.float32).reshape(-1)
         full_n[plane:(self.g.nz + 1) * plane] = np.asarray(n, np.int16).reshape(-1)
@@ -464,6 +475,6 @@ class SlabDriver:
     def owned(self):
         """(disk, n) of the owned planes as host arrays (after finish())."""
         d, n = self.ctx.copy_out()
-        plane = self.g.cps * self.g.cps
+        plane = self.g.cps * self.cps_y
         row = 3 * self.g.nmax
         return d[plane * row:(self.g.nz + 1) * plane * row], n[plane:(self.g.nz + 1) * plane]

@@ -1,0 +1,169 @@
+"""The product slab driver (pmc_slab_sweep, C) at world sizes > 1 on ONE GPU.
+
+W slab contexts live in one process, one host thread per rank, and exchange their halos through
+the in-process transport (pmc_local_group): the same schedule, streams, events, peers and message
+lists the driver hands to RCCL on a multi-GPU node, carried as device-to-device copies.  Each W is
+compared bit for bit with the C oracle's whole-box run (every occupied slot, counts, the four
+counters; the energy to rounding of the per-slab sums), over sweeps that shift along x, y and z
+in both directions (start.cu:237-260 is the loop being partitioned), plus a snapshot restart.
+Tolerance: none for state and counters.
+"""
+import os
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _run_ranks(world, fn, timeout=240):
+    """fn(rank) in one thread per rank; re-raise the first failure."""
+    out, err = [None] * world, [None] * world
+
+    def body(r):
+        try:
+            out[r] = fn(r)
+        except BaseException as e:  # noqa: BLE001 -- reported below
+            err[r] = e
+
+    th = [threading.Thread(target=body, args=(r,), daemon=True) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout)
+    assert not any(t.is_alive() for t in th), "a rank thread is still running"
+    for e in err:
+        if e is not None:
+            raise e
+    return out
+
+
+def _window(oracle, count):
+    """First sweep s of a window [s, s+count) whose plans shift along x, y, and z both ways."""
+    for s in range(0, 400):
+        plans = [oracle.sweep_plan(1234, s + k, 2.5) for k in range(count)]
+        fs = {f for _, f, _ in plans}
+        zdirs = {d > 0 for _, f, d in plans if f == 2}
+        if fs == {0, 1, 2} and zdirs == {True, False}:
+            return s
+    raise AssertionError("no window")
+
+
+@pytest.mark.parametrize("world,cps,cps_y,cps_z,atoms", [
+    (2, 16, 16, 16, 10_000),
+    (3, 16, 16, 12, 7_500),
+    (4, 16, 16, 16, 10_000),
+    (8, 16, 16, 16, 10_000),      # 2 planes per rank: no interior launch at all
+    (4, 32, 32, 32, 120_000),
+    (2, 12, 20, 16, 9_000),      # rectangular x/y
+])
+def test_c_slab_driver_world_equals_oracle(pmc, oracle, world, cps, cps_y, cps_z, atoms):
+    from pmc_amd.engine import LocalGroup
+    from pmc_amd.slab import SlabDriver
+    nz = cps_z // world
+    count = 8
+    first = _window(oracle, count)
+    pmc.lib()
+    group = LocalGroup(world)
+    drivers = [None] * world
+
+    def rank_main(r):
+        d = SlabDriver(cps=cps, cps_y=cps_y, nz_local=nz, rank=r, world=world, atoms_total=atoms,
+                       local_group=group)
+        drivers[r] = d
+        d.run(first, count)
+        d.ctx.synchronize()
+        return d.owned(), d.ctx.stats(), d.ctx.energy(), d.ctx.error_flags()
+
+    res = _run_ranks(world, rank_main)
+    st = oracle.OracleState(oracle.make_params(cps=cps, cps_y=cps_y, cps_z=cps_z))
+    assert st.init_lattice(atoms) == 0
+    assert st.run(first, count) == 0
+    plane, row = cps * cps_y, 3 * 16
+    tot = {"de_fixed": 0, "accepted": 0, "trials": 0, "evaluated": 0}
+    e_sum = 0.0
+    for r, ((d, n), s, e, fl) in enumerate(res):
+        ref = slice(r * nz * plane, (r + 1) * nz * plane)
+        assert np.array_equal(n, st.n[ref]), f"rank {r}: counts differ"
+        assert oracle.valid_slots_equal(d, n, st.disk[ref.start * row:ref.stop * row], st.n[ref], 16), \
+            f"rank {r}: coordinates differ"
+        assert fl == 0
+        for k in tot:
+            tot[k] += s[k]
+        e_sum += e
+    assert tot == st.stats.as_dict()
+    assert int(sum(int(n.sum()) for (_, n), *_ in res)) == atoms
+    assert e_sum == pytest.approx(st.energy(), rel=1e-9, abs=1e-9)
+    for d in drivers:
+        d.ctx.close()
+    group.close()
+
+
+def test_c_slab_driver_world3_restart(pmc, oracle, tmp_path):
+    """Per-rank snapshots + halo refill through the in-process transport: a fresh group restored
+    from the snapshots repeats the last sweeps bit for bit."""
+    from pmc_amd.engine import LocalGroup
+    from pmc_amd.slab import SlabDriver
+    world, cps, cps_z, atoms = 3, 16, 12, 7_500
+    nz = cps_z // world
+    first = _window(oracle, 6)
+    pmc.lib()
+    group = LocalGroup(world)
+    paths = [str(tmp_path / f"rank{r}.pmcsnap") for r in range(world)]
+    keep = []
+
+    def part1(r):
+        d = SlabDriver(cps=cps, nz_local=nz, rank=r, world=world, atoms_total=atoms, local_group=group)
+        keep.append(d)
+        d.run(first, 3)
+        d.ctx.save_snapshot(paths[r], first + 3)
+        d.run(first + 3, 3)
+        return d.owned(), d.ctx.stats()
+
+    a = _run_ranks(world, part1)
+    for d in keep:
+        d.ctx.close()
+    group.close()
+    group2 = LocalGroup(world)
+    keep2 = []
+
+    def part2(r):
+        d = SlabDriver(cps=cps, nz_local=nz, rank=r, world=world, local_group=group2)
+        keep2.append(d)
+        s = d.ctx.load_snapshot(paths[r])
+        d.ctx.slab_exchange()
+        d.run(s, 3)
+        return d.owned(), d.ctx.stats()
+
+    b = _run_ranks(world, part2)
+    for r in range(world):
+        (d1, n1), s1 = a[r]
+        (d2, n2), s2 = b[r]
+        assert np.array_equal(n1, n2)
+        assert oracle.valid_slots_equal(d1, n1, d2, n2, 16)
+        assert s1 == s2
+    for d in keep2:
+        d.ctx.close()
+    group2.close()
+
+
+def test_local_group_missing_rank_fails_not_hangs(pmc):
+    """A rank that never joins an exchange breaks the group after the barrier timeout: the caller
+    gets an error instead of a hang."""
+    from pmc_amd.engine import LocalGroup
+    from pmc_amd._lib import PmcError
+    from pmc_amd.slab import SlabDriver
+    pmc.lib()
+    os.environ["PMC_LOCAL_GROUP_TIMEOUT_MS"] = "1500"
+    try:
+        group = LocalGroup(2)
+    finally:
+        del os.environ["PMC_LOCAL_GROUP_TIMEOUT_MS"]
+    d = SlabDriver(cps=16, nz_local=8, rank=0, world=2, local_group=group)
+    with pytest.raises(PmcError):
+        d.ctx.slab_exchange()
+    with pytest.raises(PmcError):   # the group stays broken
+        d.ctx.slab_exchange()
+    d.ctx.close()
+    group.close()
