@@ -1,23 +1,30 @@
 """bench.py -- MC trial-moves/s of the checkerboard Metropolis hot path on MI355X.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--cps 128] [--atoms 10000000]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 3|4|5|5box]
   torchrun --nproc-per-node N bench.py --gpus N ...     (one rank per GPU, z-slab decomposition)
 
-A "step" is one full MC sweep (8 checkerboard colour phases + shiftCells) of BASELINE.json
-config 3 (128^3 cells, 1e7 particles per GPU, w=rc=2.5, beta=0.3, sigma=0.5, n_M=10, nmax=16,
-Philox seed 1234, reference lattice start) with the state resident in HBM.  With N>1 ranks every
-rank owns a 128^3-cell slab of a 128x128x(128N) periodic box (weak scaling; the 8-rank point has
-the per-GPU work of config 5) and exchanges halo planes with its z-neighbours over RCCL.
---strong runs BASELINE config 4 instead: ONE 128^3 box with 1e7 particles split into N slabs of
-128/N planes (the 1-GPU state, plane for plane), "scaling": "strong".
+A "step" is one full MC sweep (8 checkerboard colour phases + shiftCells) with the state resident
+in HBM; w=rc=2.5, beta=0.3, sigma=0.5, n_M=10, nmax=16, Philox seed 1234, reference lattice start
+(kernel.cu:78-89).  The workloads are BASELINE.json's configs:
 
-Rank 0 prints ONE JSON line with value = trial moves per second over all ranks, the roofline of
-the dominant kernel (subsweep; algorithmic bytes per launch / HIP-event launch time vs 8 TB/s)
-and the CPU baseline (the C oracle, OpenMP over the cells of a colour, on a bounded sample).
+  3     (default at N=1)  128^3 cells, 1e7 particles, 1 GPU, whole periodic box.
+  4     (default at N>1)  the SAME 128^3 / 1e7 box split into N z-slabs of 128/N planes (strong
+                          scaling; the C slab driver, halo planes over RCCL).  N=1 runs config 3.
+  5                       weak scaling: per GPU a 256x256x32 slab of the 256^3 / 8e7 box (its planes
+                          of the 8e7 lattice), box 256x256x(32N); at N=8 exactly config 5.  At N=1
+                          the halos travel through a one-rank RCCL communicator (rehearsal).
+  5box                    the whole 256^3 / 8e7 box on one GPU.
+
+Rank 0 prints ONE JSON line: value = trial moves per second over all ranks; the roofline of the
+dominant kernel (subsweep: algorithmic bytes per launch / HIP-event launch time vs 8 TB/s); the
+CPU baseline (the C oracle: serial on one core and OpenMP over the cells of a colour on one
+socket's cores, bounded samples, host CPU described); and the parity leg (the CPU sample's sweep
+rerun on the GPU and compared with the oracle bit for bit).
 """
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -29,6 +36,15 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "parallel-monte-carlo_amd"))
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+CONFIG_NAMES = {
+    "3": "BASELINE config 3: 128^3 cells, 1e7 particles, 1 MI355X, full checkerboard + shiftCells",
+    "4": "BASELINE config 4: 128^3 cells, 1e7 particles, {n} MI355X, checkerboard domain decomposition "
+         "+ RCCL halo (strong scaling: {n} z-slabs of {nz} planes)",
+    "5": "BASELINE config 5: 256^3 cells, 8e7 particles, 8 MI355X weak-scaling -- per GPU a 256x256x32 "
+         "slab with its 1e7 particles of the 8e7 lattice; box 256x256x{cz} at {n} GPU(s)",
+    "5box": "256^3 cells, 8e7 particles (the config-5 box) whole on 1 MI355X",
+}
 
 
 def stencil_counts(n: np.ndarray, cps: tuple[int, int, int]) -> np.ndarray:
@@ -43,30 +59,122 @@ def stencil_counts(n: np.ndarray, cps: tuple[int, int, int]) -> np.ndarray:
     return s.reshape(-1)
 
 
-def algorithmic_bytes_per_sweep(n_owned: np.ndarray, stencil: np.ndarray) -> dict:
-    """SURVEY.md 8(d) staged model: per visited (non-empty) cell read its 27-cell stencil
-    (12 B per particle), 27 counts (2 B each) and write its own particles (12 B each)."""
-    ne = n_owned > 0
-    sub = float(np.sum(12 * stencil[ne] + 54 + 12 * n_owned[ne]))
-    shift = float(np.sum(36 * n_owned.astype(np.int64) + 6)) * 1.0
-    return {"subsweep_sweep": sub, "subsweep_launch": sub / 8.0, "shift": shift}
+def slab_stencil_counts(n_storage: np.ndarray, cps: int, nz: int) -> np.ndarray:
+    """S_c of the owned cells of a slab (storage planes 0 and nz+1 are the halos)."""
+    g = n_storage.astype(np.int64).reshape(nz + 2, cps, cps)
+    s = np.zeros((nz, cps, cps), np.int64)
+    for dz in (-1, 0, 1):
+        sub = g[1 + dz:1 + dz + nz]
+        for dy in (-1, 0, 1):
+            for dx in (-1, 0, 1):
+                s += np.roll(sub, shift=(-dy, -dx), axis=(1, 2))
+    return s.reshape(-1)
 
 
-def cpu_baseline(disk: np.ndarray, n: np.ndarray, cps: int, sweeps: int, threads: int, sweep0: int) -> dict:
+def staged_bytes(n_cells: np.ndarray, stencil: np.ndarray) -> float:
+    """SURVEY.md 8(d) staged model for a set of cell visits: per visited (non-empty) cell read its
+    27-cell stencil (12 B per particle), 27 counts (2 B each) and write its own particles (12 B each)."""
+    ne = n_cells > 0
+    return float(np.sum(12 * stencil[ne] + 54 + 12 * n_cells[ne]))
+
+
+# ---- host CPU description (SURVEY.md 8d: nproc, model, sockets, cores used) ------------------
+def _read(path: str) -> str | None:
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def host_cpu() -> dict:
+    model = None
+    txt = _read("/proc/cpuinfo") or ""
+    for line in txt.splitlines():
+        if line.startswith("model name"):
+            model = line.split(":", 1)[1].strip()
+            break
+    allowed = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
+    topo = {}
+    for cpu_dir in glob.glob("/sys/devices/system/cpu/cpu[0-9]*"):
+        cpu = int(cpu_dir.rsplit("cpu", 1)[1])
+        pkg = _read(f"{cpu_dir}/topology/physical_package_id")
+        core = _read(f"{cpu_dir}/topology/core_id")
+        if pkg is not None and core is not None:
+            topo[cpu] = (int(pkg), int(core))
+    sockets = sorted({p for p, _ in topo.values()}) or [0]
+    cores_per_socket = {s: len({c for p, c in topo.values() if p == s}) for s in sockets}
+    # one logical CPU per physical core of socket 0 among the CPUs this process may run on
+    first_socket = sockets[0]
+    seen, socket0_cpus = set(), []
+    for cpu in allowed:
+        key = topo.get(cpu)
+        if key and key[0] == first_socket and key not in seen:
+            seen.add(key)
+            socket0_cpus.append(cpu)
+    quota = None
+    cm = _read("/sys/fs/cgroup/cpu.max")
+    if cm and not cm.startswith("max"):
+        q, per = cm.split()[:2]
+        quota = float(q) / float(per)
+    return {"model": model, "logical_cpus": os.cpu_count(), "affinity_cpus": len(allowed),
+            "sockets": len(sockets), "cores_per_socket": cores_per_socket.get(first_socket),
+            "socket0_cores_allowed": len(socket0_cpus), "cgroup_cpu_quota": quota,
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
+
+
+def cpu_baseline(disk, n, cps: int, sweep0: int, serial_planes: int) -> tuple[dict, object]:
+    """The C oracle (the reference has no CPU path: SURVEY.md 0/8c) timed on this host:
+    (i) serial, one core: one colour phase over planes [0, serial_planes);
+    (ii) OpenMP over the cells of a colour on the cores of one socket (one thread per physical
+    core, limited by the CPUs/cgroup quota this process may use): one full sweep from the GPU
+    state.  Returns the JSON object and the oracle state after (ii) for the parity leg."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import pmc_oracle  # test infrastructure: timed CPU baseline only
     pmc_oracle.build()
+    host = host_cpu()
+    # (i) serial
+    st1 = pmc_oracle.OracleState(pmc_oracle.make_params(cps=cps))
+    st1.disk[:] = disk
+    st1.n[:] = n
+    pmc_oracle.set_threads(1)
+    import ctypes as C
+    t0 = time.perf_counter()
+    pmc_oracle.lib().orc_subsweep_range(C.byref(st1.p), st1.disk, st1.n, 0, 0, 0, sweep0, 0, serial_planes,
+                                        C.byref(st1.stats))
+    dt1 = time.perf_counter() - t0
+    serial = st1.stats.trials / dt1
+    del st1
+    # (ii) one socket
+    threads = host["socket0_cores_allowed"] or 1
+    limited_by = "socket cores"
+    if host["cgroup_cpu_quota"] and host["cgroup_cpu_quota"] < threads:
+        threads = max(1, int(host["cgroup_cpu_quota"]))
+        limited_by = "cgroup CPU quota"
     st = pmc_oracle.OracleState(pmc_oracle.make_params(cps=cps))
     st.disk[:] = disk
     st.n[:] = n
-    pmc_oracle.set_threads(threads)
+    used = pmc_oracle.set_threads(threads)
     t0 = time.perf_counter()
-    st.run(sweep0, sweeps)
+    st.run(sweep0, 1)
     dt = time.perf_counter() - t0
-    trials = st.stats.trials
-    return {"value": trials / dt, "unit": "trial-moves/s", "cores": threads, "kind": "port",
-            "sample": f"{sweeps} full sweep(s) of the {cps}^3-cell box from the GPU state "
-                      f"(C oracle, OpenMP over cells of a colour, {threads} threads), {dt:.2f} s"}, st
+    par = st.stats.trials / dt
+    cores_socket = host["cores_per_socket"] or threads
+    out = {"value": par, "unit": "trial-moves/s", "cores": threads, "kind": "port",
+           "sample": f"one full sweep of the {cps}^3 box from the GPU state, C oracle, OpenMP over the cells "
+                     f"of a colour on {threads} threads (one per physical core of socket 0; limited by "
+                     f"{limited_by}), {dt:.2f} s",
+           "serial": {"value": serial, "cores": 1,
+                      "sample": f"one colour phase over planes [0,{serial_planes}) of the {cps}^3 box, 1 thread, "
+                                f"{dt1:.2f} s"},
+           "parallel_efficiency": par / (serial * threads),
+           "socket_cores": cores_socket,
+           "socket_estimate": (par * cores_socket / threads) if threads < cores_socket else par,
+           "socket_estimate_note": ("measured" if threads >= cores_socket else
+                                    f"linear extrapolation of the measured {threads}-thread rate to the "
+                                    f"{cores_socket} cores of one socket (upper bound)"),
+           "omp_threads_reported": used, "host": host}
+    return out, st
 
 
 def parity_leg(sim, one_sweep, disk0, n0, sweep0: int, sweeps: int, e0: float, ost) -> dict:
@@ -78,7 +186,7 @@ def parity_leg(sim, one_sweep, disk0, n0, sweep0: int, sweeps: int, e0: float, o
     sim.copy_in(disk0, n0)
     sim.stats(reset=True)
     for k in range(sweeps):
-        one_sweep(sweep0 + k, False)
+        one_sweep(sweep0 + k)
     sim.synchronize()
     g = sim.stats()
     e_gpu = sim.energy()
@@ -88,7 +196,7 @@ def parity_leg(sim, one_sweep, disk0, n0, sweep0: int, sweeps: int, e0: float, o
     same = bool(np.array_equal(n_g, ost.n)) and pmc_oracle.valid_slots_equal(disk_g, n_g, ost.disk, ost.n, ost.nmax)
     acc_g = g["accepted"] / g["trials"] if g["trials"] else 0.0
     acc_c = c["accepted"] / c["trials"] if c["trials"] else 0.0
-    rel = lambda a, b: abs(a - b) / abs(b) if b else abs(a - b)
+    rel = lambda a, b: abs(a - b) / abs(b) if b else abs(a - b)  # noqa: E731
     return {"reference": "C oracle (corrected-mode restatement of subsweep.h / shiftCells.h)",
             "sweeps": sweeps, "first_sweep": sweep0, "energy_start": e0,
             "energy_gpu": e_gpu, "energy_cpu": e_cpu, "energy_rel_err": rel(e_gpu, e_cpu),
@@ -112,23 +220,21 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--cps", type=int, default=128)
-    ap.add_argument("--atoms", type=int, default=10_000_000)
-    ap.add_argument("--cpu-sweeps", type=int, default=1)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--config", choices=["3", "4", "5", "5box"], default=None,
+                    help="BASELINE config (default: 3 at N=1, 4 at N>1)")
+    ap.add_argument("--strong", action="store_true", help="alias of --config 4")
+    ap.add_argument("--cps", type=int, default=None, help="override cells per side (configs 3/4)")
+    ap.add_argument("--atoms", type=int, default=None, help="override the particle count (configs 3/4)")
+    ap.add_argument("--serial-planes", type=int, default=None,
+                    help="planes of the serial CPU sample's colour phase (default: the whole box up to 128)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--graph", action="store_true", help="replay the timed sweeps as one hipGraph")
     ap.add_argument("--no-events", action="store_true",
                     help="no per-launch HIP events in the timed region (no roofline; overhead check)")
-    ap.add_argument("--slab", action="store_true", help="use the z-slab/halo path even with one rank")
-    ap.add_argument("--slab-driver", choices=["c", "python"], default="c",
-                    help="multi-GPU driver: the C slab driver with RCCL (product) or the Python schedule "
-                         "over torch.distributed")
+    ap.add_argument("--slab", action="store_true", help="config 3 through the z-slab driver with one rank")
     ap.add_argument("--self-rccl", action="store_true",
-                    help="one rank with --slab: halos through a one-rank RCCL communicator (rehearsal)")
-    ap.add_argument("--strong", action="store_true",
-                    help="strong scaling (BASELINE config 4): one cps^3 box of --atoms particles split into "
-                         "world z-slabs of cps/world planes (default: weak, cps^3 and --atoms per GPU)")
+                    help="one slab rank: halos through a one-rank RCCL communicator (default for config 5)")
+    ap.add_argument("--local-halo", action="store_true", help="config 5 at N=1: local halo copies, no RCCL")
     args = ap.parse_args()
 
     import torch
@@ -140,45 +246,45 @@ def main() -> int:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}", file=sys.stderr)
+    config = args.config or ("4" if args.strong else ("3" if world == 1 else "4"))
+    if config == "4" and world == 1 and not args.slab:
+        config = "3"          # the 1-GPU point of the config-4 strong-scaling curve is config 3
+    if config == "5box" and world > 1:
+        raise SystemExit("--config 5box is the single-GPU 256^3 box")
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     stream = torch.cuda.Stream()
-    cps = args.cps
 
     def barrier():
         if world > 1:
             dist.barrier()
 
-    slab = world > 1 or args.slab
-    nz_local = cps // world if args.strong else cps
-    # weak: a lattice of --atoms per cps^3 of slab; strong: ONE lattice of --atoms over the whole
-    # box, each rank keeping its planes (the 1-GPU config 3 state, split)
-    atoms_local = args.atoms * nz_local // cps
-    if slab and (nz_local % 2 or nz_local < 2):
+    if config in ("3", "4"):
+        cps = args.cps or 128
+        atoms = args.atoms or 10_000_000
+    else:
+        cps, atoms = 256, 80_000_000
+    slab = config in ("4", "5") or args.slab
+    if config == "4" or (config == "3" and slab):
+        nz_local = cps // world
+        box_z = cps
+    elif config == "5":
+        nz_local = 32
+        box_z = 32 * world
+    else:
+        nz_local = box_z = cps
+    if slab and (nz_local % 2 or nz_local < 2 or (config == "4" and cps % world)):
         raise SystemExit(f"slab thickness {nz_local} must be even and >= 2")
-    events = []      # (kind, start, end) HIP events on the kernels' stream
-
-    def timer(kind, fn, record, on=None):
-        """HIP events around one launch, on the stream it is launched on (default: the kernels')."""
-        if not record or args.no_events:
-            return fn()
-        st = on if on is not None else stream
-        a = torch.cuda.Event(enable_timing=True)
-        b = torch.cuda.Event(enable_timing=True)
-        a.record(st)
-        fn()
-        b.record(st)
-        events.append((kind, a, b))
 
     if not slab:
         sim = pmc_amd.PmcContext(cps, stream=stream.cuda_stream)
-        sim.init_lattice(args.atoms)
+        sim.init_lattice(atoms)
         from pmc_amd.plan import sweep_plan
         plans = {}
 
-        def one_sweep(s, record):
+        def one_sweep(s):
             if s not in plans:
                 plans[s] = sweep_plan(1234, s, 2.5)
             for colour in plans[s][0]:
@@ -187,65 +293,50 @@ def main() -> int:
 
         def finish():
             pass
-        cps_z = cps
-    elif args.slab_driver == "c":
+        transport = "single GPU"
+    else:
         # the product multi-GPU path: sweep schedule + RCCL halo exchange in C (pmc_slab_*)
         from pmc_amd.slab import SlabDriver
-        drv = SlabDriver(cps=cps, nz_local=nz_local, rank=rank, world=world, stream=stream,
-                         atoms_per_rank=0 if args.strong else atoms_local,
-                         atoms_total=args.atoms if args.strong else 0, use_rccl=world > 1 or args.self_rccl)
+        use_rccl = world > 1 or args.self_rccl or (config == "5" and not args.local_halo)
+        drv = SlabDriver(cps=cps, nz_local=nz_local, rank=rank, world=world, stream=stream, use_rccl=use_rccl)
+        if config == "5":
+            drv.ctx.init_lattice_planes(atoms, cps)     # this rank's planes of the 256^3 / 8e7 lattice
+        else:
+            drv.ctx.init_lattice_global(atoms)         # this rank's planes of the one 128^3 box
+        drv.ctx.slab_exchange()
         sim = drv.ctx
 
-        def one_sweep(s, record):
+        def one_sweep(s):
             drv.sweep(s)
 
         finish = drv.finish
-        cps_z = nz_local * world
-    else:
-        # the same schedule in Python over torch.distributed (comparison)
-        from pmc_amd.slab import SlabSimulation
-        sim_s = SlabSimulation.create(cps=cps, nz_local=nz_local, rank=rank, world=world, stream=stream,
-                                      atoms_per_rank=0 if args.strong else atoms_local,
-                                      atoms_total=args.atoms if args.strong else 0)
-        sim = sim_s.ctx
-
-        def one_sweep(s, record):
-            sim_s.sweep(s, timer=lambda kind, fn, on=None: timer(kind, fn, record, on))
-
-        finish = sim_s.finish
-        cps_z = nz_local * world
-    c_slab = slab and args.slab_driver == "c"
+        transport = (f"z-slab x{world}, {nz_local} planes per rank, halo planes over "
+                     + ("RCCL (C slab driver)" if use_rccl else "local copies (C slab driver)"))
 
     # warmup
     for s in range(args.warmup):
-        one_sweep(s, False)
+        one_sweep(s)
     finish()
     torch.cuda.synchronize()
     sim.stats(reset=True)
     # algorithmic bytes from the state at the start of the timed region
     disk_h, n_h = sim.copy_out()
     plane = cps * cps
-    lo = plane if slab else 0
-    nzl = nz_local if slab else cps
-    n_owned = n_h[lo:lo + plane * nzl].astype(np.int64)
     if not slab:
+        n_owned = n_h.astype(np.int64)
         stencil = stencil_counts(n_owned, (cps, cps, cps))
+        sub_launch_bytes = staged_bytes(n_owned, stencil) / 8.0
+        roof_kernel = "k_subsweep<16,16,true> (one colour phase of the whole box)"
     else:
-        ext = n_h.astype(np.int64).reshape(nzl + 2, cps, cps)
-        g = ext
-        s = np.zeros((nzl, cps, cps), np.int64)
-        for dz in (-1, 0, 1):
-            sub = g[1 + dz:1 + dz + nzl]
-            for dy in (-1, 0, 1):
-                for dx in (-1, 0, 1):
-                    s += np.roll(sub, shift=(-dy, -dx), axis=(1, 2))
-        stencil = s.reshape(-1)
-    abytes = algorithmic_bytes_per_sweep(n_owned, stencil)
+        n_owned = n_h[plane:plane * (nz_local + 1)].astype(np.int64)
+        stencil = slab_stencil_counts(n_h, cps, nz_local)
+        # the context-stream launches are the interior planes [1, nz-1): each cell once per sweep
+        inner = slice(plane, plane * (nz_local - 1))
+        sub_launch_bytes = staged_bytes(n_owned[inner], stencil[inner]) / 8.0
+        roof_kernel = "k_subsweep<16,16,true> (interior planes of a slab colour phase)"
     e_start = sim.energy()      # cell-list energy of the state the timed region starts from
 
-    c_events = not slab or c_slab      # kernel launches from C: events on their dispatch packets
-    if c_events:
-        sim.timing(not args.no_events)
+    sim.timing_kinds(not args.no_events and not args.graph)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -254,22 +345,14 @@ def main() -> int:
         sim.run_graph(first, args.steps)
     else:
         for k in range(args.steps):
-            one_sweep(first + k, True)
+            one_sweep(first + k)
         finish()
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
     st = sim.stats()
+    tm = sim.timing_kinds(False)
     trials_local = st["trials"]
-    # kernel time of one colour phase = sum of its launches (the slab path splits a phase into the
-    # interior and the two boundary planes); 8 phases per sweep
-    phase_total_ms = sum(a.elapsed_time(b) for kind, a, b in events if kind == "phase")
-    shift_total_ms = sum(a.elapsed_time(b) for kind, a, b in events if kind == "shift")
-    n_phases = 8 * args.steps if events else 0
-    if c_events:
-        tm = sim.timing(False)
-        phase_total_ms, shift_total_ms = tm["subsweep_ms"], tm["shift_ms"]
-        n_phases = 8 * args.steps if tm["n_subsweep"] else 0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -289,28 +372,37 @@ def main() -> int:
         ev = torch.tensor([e_start, e_end, de_timed], dtype=torch.float64, device="cuda")
         dist.all_reduce(ev)
         e_start, e_end, de_timed = (float(v) for v in ev.tolist())
+    particles = int(n_owned.sum())
+    if world > 1:
+        pt = torch.tensor([particles], dtype=torch.int64, device="cuda")
+        dist.all_reduce(pt)
+        particles = int(pt.item())
 
     if rank == 0:
-        avg_launch_s = (phase_total_ms / n_phases * 1e-3) if n_phases else None
-        achieved = (abytes["subsweep_launch"] / avg_launch_s / 1e9) if avg_launch_s else None
+        n_launch = tm["n_subsweep"]
+        avg_launch_s = (tm["subsweep_ms"] / n_launch * 1e-3) if n_launch else None
+        achieved = (sub_launch_bytes / avg_launch_s / 1e9) if avg_launch_s else None
         traffic = traffic_from_profile()
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                "traffic": traffic.get("subsweep_bytes_per_launch") if traffic else None,
-                "kernel": "k_subsweep<16> (one colour phase)",
+                "traffic": traffic.get("subsweep_bytes_per_launch") if (traffic and not slab) else None,
+                "kernel": roof_kernel,
                 "launch_ms": avg_launch_s * 1e3 if avg_launch_s else None,
-                "shift_ms": shift_total_ms / args.steps if n_phases else None,
-                "algorithmic_bytes_per_launch": abytes["subsweep_launch"]}
+                "launches_timed": n_launch,
+                "shift_ms": tm["shift_ms"] / tm["n_shift"] if tm["n_shift"] else None,
+                "boundary_launch_ms": tm["boundary_ms"] / tm["n_boundary"] if tm["n_boundary"] else None,
+                "algorithmic_bytes_per_launch": sub_launch_bytes}
         cpu = None
         parity = None
         if not args.no_cpu_baseline and not slab:
             try:
-                thr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-                cpu, ost = cpu_baseline(disk_h, n_h, cps, args.cpu_sweeps, thr, first)
-                parity = parity_leg(sim, one_sweep, disk_h, n_h, first, args.cpu_sweeps, e_start, ost)
+                sp = args.serial_planes or min(cps, 128)
+                cpu, ost = cpu_baseline(disk_h, n_h, cps, first, sp)
+                parity = parity_leg(sim, one_sweep, disk_h, n_h, first, 1, e_start, ost)
             except Exception as e:  # the baseline is reported, never the measured value
                 cpu = {"error": repr(e)}
         sweeps_per_s = args.steps / elapsed
+        name = CONFIG_NAMES[config].format(n=world, nz=nz_local, cz=box_z)
         out = {
             "metric": "MC trial-moves/s (whole node)",
             "value": value,
@@ -320,25 +412,20 @@ def main() -> int:
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "strong" if args.strong else "weak",
+            "scaling": "strong" if config == "4" else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (reference simple-cubic lattice start, Philox seed 1234)",
-            "config": {"workload": (f"{cps}^3 cells x {args.atoms:.0e} particles in total" if args.strong else
-                                    f"{cps}x{cps}x{nzl} cells x {atoms_local:.0e} particles per GPU") +
-                                   f", full checkerboard sweep (8 colour phases + shiftCells), box {cps}x{cps}x{cps_z}",
-                       "cells_per_gpu": cps * cps * nzl, "particles_per_gpu": atoms_local, "n_moves": 10,
-                       "nmax": 16, "beta": 0.3, "sigma": 0.5, "w": 2.5,
-                       "parallelism": (f"z-slab x{world}, {nzl} planes per rank, halo planes over "
-                                       + ("RCCL (C driver)" if c_slab and (world > 1 or args.self_rccl) else
-                                          "local copies (C driver)" if c_slab else "torch.distributed"))
-                                      if slab else "single GPU"},
+            "config": {"workload": name, "baseline_config": config,
+                       "box_cells": [cps, cps, box_z], "cells_per_gpu": cps * cps * nz_local,
+                       "particles": particles, "n_moves": 10, "nmax": 16, "beta": 0.3, "sigma": 0.5,
+                       "w": 2.5, "parallelism": transport},
             "sweeps_per_s": sweeps_per_s,
             "acceptance": st["accepted"] / st["trials"] if st["trials"] else None,
             "energy": {"start": e_start, "end": e_end, "start_plus_sum_dE": e_start + de_timed,
-                       "per_particle_end": e_end / (atoms_local * world),
+                       "per_particle_end": e_end / particles if particles else None,
                        "bookkeeping_rel_err": abs(e_start + de_timed - e_end) / abs(e_end) if e_end else None,
-                       "particles": atoms_local * world},
+                       "particles": particles},
             "parity": parity,
             "error_flags": flags,
             "roofline": roof,

@@ -123,6 +123,13 @@ int pmc_init_lattice(pmc_ctx* ctx, int64_t n_atoms);
  * owned planes equal the same planes of a whole-box pmc_init_lattice, slot for slot.  With no
  * slab (z0 = 0, nz_local = cps_z) it is pmc_init_lattice. */
 int pmc_init_lattice_global(pmc_ctx* ctx, int64_t n_atoms_total);
+/* The reference lattice of n_atoms_lattice particles over a TALLER box of cps_x x cps_y x
+ * lattice_cps_z cells (init_r, kernel.cu:78-89), bottom-aligned with the periodic box; the rows
+ * inside the box's planes [0, cps_z) are kept, this slab keeping its owned planes.  The config-5
+ * weak-scaling start (bench.py --config 5): N ranks of 256x256x32 cells hold exactly the planes
+ * they hold in the 8-rank 256^3 / 8e7 box.  lattice_cps_z == cps_z (or 0) is
+ * pmc_init_lattice_global. */
+int pmc_init_lattice_planes(pmc_ctx* ctx, int64_t n_atoms_lattice, int32_t lattice_cps_z);
 /* One full MC sweep on the context state: colour order from the sweep plan, 8 subsweeps,
  * shiftCells, buffer swap (start.cu:237-260).  Asynchronous. */
 int pmc_sweep(pmc_ctx* ctx, uint32_t sweep);
@@ -189,10 +196,14 @@ int pmc_slab_sweep(pmc_ctx* ctx, uint32_t sweep);
 int pmc_slab_finish(pmc_ctx* ctx);
 /* Sum of the HIP-event durations of the subsweep and shift launches since the last call
  * (synchronizes), then switch per-launch events on (enable = 1) or off.  The events ride on the
- * kernels' own dispatch packets (no extra packets between launches); graph replays are not timed.
- * pmc_timing covers every launch of the context; pmc_slab_timing is the same call, requiring the
- * slab driver. */
+ * kernels' own dispatch packets (no extra packets between launches); graph replays and the
+ * overflow (fallback) launches are not timed.  pmc_timing reports the subsweep launches on the
+ * context stream (the slab driver's interior planes) and the shift launches; pmc_slab_timing is the
+ * same call, requiring the slab driver.  pmc_timing_kinds splits by kind: [0] subsweep launches on
+ * the context stream, [1] shiftCells, [2] subsweep launches on another stream (the slab driver's
+ * boundary planes, which run concurrently with [0]: their durations overlap and do not add). */
 int pmc_timing(pmc_ctx* ctx, int enable, double* subsweep_ms, int* n_subsweep, double* shift_ms, int* n_shift);
+int pmc_timing_kinds(pmc_ctx* ctx, int enable, double ms[3], int count[3]);
 int pmc_slab_timing(pmc_ctx* ctx, int enable, double* subsweep_ms, int* n_subsweep, double* shift_ms,
                     int* n_shift);
 /* The per-sweep plan every rank replicates (no broadcast): colour order (FY_Shuffle + itoa,

@@ -47,7 +47,7 @@ struct pmc_ctx {
     // per-launch kernel timing (pmc_timing): dispatch-packet events, (start, stop) pairs in use
     bool timing = false;
     std::vector<hipEvent_t> tev;
-    std::vector<int> tkind;                // 0 subsweep, 1 shift
+    std::vector<int> tkind;                // 0 subsweep (context stream), 1 shift, 2 subsweep (aux stream)
     uint32_t graph_first = 0;
     int graph_count = 0;
     int graph_cur = -1;
@@ -383,20 +383,23 @@ int pmc_init_lattice(pmc_ctx* c, int64_t n_atoms) {
     return pmc_assign(c, c->d_r, n_atoms, c->disk[c->cur], c->n[c->cur]);
 }
 
-int pmc_init_lattice_global(pmc_ctx* c, int64_t n_atoms_total) {
-    if (!c || n_atoms_total < 0) return fail(PMC_ERR_ARG, "bad argument");
-    if (n_atoms_total > c->r_cap) {
+int pmc_init_lattice_planes(pmc_ctx* c, int64_t n_atoms_lattice, int32_t lattice_cps_z) {
+    if (!c || n_atoms_lattice < 0) return fail(PMC_ERR_ARG, "bad argument");
+    if (lattice_cps_z == 0) lattice_cps_z = c->P.cps_z;
+    if (lattice_cps_z < c->P.cps_z) return fail(PMC_ERR_ARG, "lattice box lower than the simulation box");
+    if (n_atoms_lattice > c->r_cap) {
         if (c->d_r) PMC_HIP(hipFree(c->d_r));
         c->d_r = nullptr;
-        PMC_HIP(hipMalloc(&c->d_r, sizeof(float) * 3 * (size_t)(n_atoms_total > 0 ? n_atoms_total : 1)));
-        c->r_cap = n_atoms_total;
+        PMC_HIP(hipMalloc(&c->d_r, sizeof(float) * 3 * (size_t)(n_atoms_lattice > 0 ? n_atoms_lattice : 1)));
+        c->r_cap = n_atoms_lattice;
     }
-    // init_r over the whole periodic box (z0 = 0, all cps_z planes): the same floats as a
-    // whole-box context's lattice
+    // init_r over the lattice box cps_x x cps_y x lattice_cps_z, bottom-aligned with the periodic
+    // box (z from -Lz/2): k_init_r's slab form with z0 = 0 and nz_local = lattice_cps_z.  With
+    // lattice_cps_z == cps_z the offset is exactly 0 and these are a whole-box context's floats.
     DevGeom gg = c->G;
     gg.z0 = 0;
-    gg.nz_local = c->P.cps_z;
-    hipError_t e = launch_init_r(gg, n_atoms_total, icbrt_ceil(n_atoms_total), c->d_r, c->stream);
+    gg.nz_local = lattice_cps_z;
+    hipError_t e = launch_init_r(gg, n_atoms_lattice, icbrt_ceil(n_atoms_lattice), c->d_r, c->stream);
     if (e != hipSuccess) return hip_fail(e, "init_r launch");
     PMC_HIP(hipMemsetAsync(c->n[c->cur], 0, n_bytes(c), c->stream));
     if (!c->tmp_cnt) {
@@ -404,9 +407,10 @@ int pmc_init_lattice_global(pmc_ctx* c, int64_t n_atoms_total) {
         PMC_HIP(hipMalloc(&c->tmp_idx, sizeof(int32_t) * (size_t)c->cells * (size_t)c->P.nmax));
     }
     PMC_HIP(hipMemsetAsync(c->flags, 0, 16, c->stream));
-    // assign keeps the owned planes' particles (clip: other slabs' particles are skipped)
-    e = launch_assign(c->G, c->d_r, n_atoms_total, c->disk[c->cur], c->n[c->cur], c->tmp_cnt, c->tmp_idx,
-                      c->flags, c->stream, 1);
+    // assign keeps the owned planes' particles (clip 1: other slabs' particles are skipped;
+    // clip 2: also the lattice rows above the periodic box)
+    e = launch_assign(c->G, c->d_r, n_atoms_lattice, c->disk[c->cur], c->n[c->cur], c->tmp_cnt, c->tmp_idx,
+                      c->flags, c->stream, lattice_cps_z > c->P.cps_z ? 2 : 1);
     if (e != hipSuccess) return hip_fail(e, "assign launch");
     uint32_t fl = 0;
     PMC_HIP(hipMemcpyAsync(&fl, c->flags, 4, hipMemcpyDeviceToHost, c->stream));
@@ -414,6 +418,11 @@ int pmc_init_lattice_global(pmc_ctx* c, int64_t n_atoms_total) {
     if (fl & 4u) return fail(PMC_ERR_RANGE, "assign: particle outside the box");
     if (fl & 2u) return fail(PMC_ERR_OVERFLOW, "assign: cell occupancy exceeds nmax");
     return PMC_OK;
+}
+
+int pmc_init_lattice_global(pmc_ctx* c, int64_t n_atoms_total) {
+    if (!c) return fail(PMC_ERR_ARG, "null ctx");
+    return pmc_init_lattice_planes(c, n_atoms_total, c->P.cps_z);
 }
 
 int pmc_phase_range(pmc_ctx* c, int colour, uint32_t sweep, int zl_begin, int zl_end) {
@@ -437,7 +446,7 @@ int pmc_phase_range_on(pmc_ctx* c, int colour, uint32_t sweep, int zl_begin, int
     pmc_colour_offset(colour, o);
     LaunchTiming lt;
     hipError_t e = launch_subsweep(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep, c->stats,
-                                   c->ovf_aux, zl_begin, zl_end, st, next_timing(c, 0, &lt));
+                                   c->ovf_aux, zl_begin, zl_end, st, next_timing(c, 2, &lt));
     return e == hipSuccess ? PMC_OK : hip_fail(e, "subsweep launch");
 }
 
@@ -1238,7 +1247,7 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
         float* mirror = s->messages() ? s->sbuf : disk_plane(c, down ? nz : -1);
         LaunchTiming lt;
         e = launch_subsweep_boundary(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep, c->stats, c->ovf_aux, zb,
-                                     zb + 1, mirror, s->messages() ? 0 : 1, T, next_timing(c, 0, &lt));
+                                     zb + 1, mirror, s->messages() ? 0 : 1, T, next_timing(c, 2, &lt));
         if (e != hipSuccess) return hip_fail(e, "subsweep launch");
         PMC_HIP(hipEventRecord(s->ev_b, T));
         // exchange k and its unpack follow B(k) on T straight away, so they run beside I(k)
@@ -1280,26 +1289,38 @@ int pmc_slab_finish(pmc_ctx* c) {
     return PMC_OK;
 }
 
-int pmc_timing(pmc_ctx* c, int enable, double* subsweep_ms, int* n_subsweep, double* shift_ms, int* n_shift) {
+int pmc_timing_kinds(pmc_ctx* c, int enable, double ms[3], int count[3]) {
     if (!c) return fail(PMC_ERR_ARG, "null ctx");
-    double a = 0.0, b = 0.0;
-    int na = 0, nb = 0;
+    double a[3] = {0.0, 0.0, 0.0};
+    int na[3] = {0, 0, 0};
     if (!c->tkind.empty()) {
         PMC_HIP(hipStreamSynchronize(c->stream));
         if (c->slab) PMC_HIP(hipStreamSynchronize(c->slab->aux));
         for (size_t k = 0; k < c->tkind.size(); ++k) {
-            float ms = 0.0f;
-            PMC_HIP(hipEventElapsedTime(&ms, c->tev[2 * k], c->tev[2 * k + 1]));
-            if (c->tkind[k] == 0) { a += ms; ++na; }
-            else { b += ms; ++nb; }
+            float t = 0.0f;
+            PMC_HIP(hipEventElapsedTime(&t, c->tev[2 * k], c->tev[2 * k + 1]));
+            a[c->tkind[k]] += t;
+            ++na[c->tkind[k]];
         }
     }
-    if (subsweep_ms) *subsweep_ms = a;
-    if (n_subsweep) *n_subsweep = na;
-    if (shift_ms) *shift_ms = b;
-    if (n_shift) *n_shift = nb;
+    for (int k = 0; k < 3; ++k) {
+        if (ms) ms[k] = a[k];
+        if (count) count[k] = na[k];
+    }
     c->tkind.clear();
     c->timing = enable != 0;
+    return PMC_OK;
+}
+
+int pmc_timing(pmc_ctx* c, int enable, double* subsweep_ms, int* n_subsweep, double* shift_ms, int* n_shift) {
+    double ms[3];
+    int cnt[3];
+    int rc = pmc_timing_kinds(c, enable, ms, cnt);
+    if (rc) return rc;
+    if (subsweep_ms) *subsweep_ms = ms[0];
+    if (n_subsweep) *n_subsweep = cnt[0];
+    if (shift_ms) *shift_ms = ms[1];
+    if (n_shift) *n_shift = cnt[1];
     return PMC_OK;
 }
 

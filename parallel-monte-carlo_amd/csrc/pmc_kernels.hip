@@ -1080,7 +1080,10 @@ __global__ void k_assign_count(DevGeom g, const float* __restrict__ r, int64_t n
     if (i >= n_atoms) return;
     const int cx = bin_axis(r[i], g.cps_x, g.w);
     const int cy = bin_axis(r[i + n_atoms], g.cps_y, g.w);
-    const int cz = bin_axis(r[i + 2 * n_atoms], g.cps_z, g.w);
+    const float zv = r[i + 2 * n_atoms];
+    // clip 2 (pmc_init_lattice_planes): lattice rows above the periodic box are not part of it
+    if (clip == 2 && zv > g.Lz / 2.0f) return;
+    const int cz = bin_axis(zv, g.cps_z, g.w);
     if (cx < 0 || cy < 0 || cz < 0) {
         atomicOr(flags, 4u);
         return;

@@ -104,6 +104,7 @@ def lib():
         _sig(L, "pmc_shift_cells", i32, _vp, _vp, _vp, _vp, _vp, i32, C.c_float)
         _sig(L, "pmc_init_lattice", i32, _vp, i64)
         _sig(L, "pmc_init_lattice_global", i32, _vp, i64)
+        _sig(L, "pmc_init_lattice_planes", i32, _vp, i64, i32)
         _sig(L, "pmc_sweep", i32, _vp, u32)
         _sig(L, "pmc_phase", i32, _vp, i32, u32)
         _sig(L, "pmc_phase_range", i32, _vp, i32, u32, i32, i32)
@@ -118,6 +119,7 @@ def lib():
         _sig(L, "pmc_slab_finish", i32, _vp)
         _sig(L, "pmc_slab_timing", i32, _vp, i32, _vp, _vp, _vp, _vp)
         _sig(L, "pmc_timing", i32, _vp, i32, _vp, _vp, _vp, _vp)
+        _sig(L, "pmc_timing_kinds", i32, _vp, i32, C.POINTER(C.c_double * 3), C.POINTER(C.c_int * 3))
         _sig(L, "pmc_subsweep_range", i32, _vp, _vp, _vp, C.POINTER(C.c_int * 3), u32, i32, i32)
         _sig(L, "pmc_shift", i32, _vp, u32)
         _sig(L, "pmc_shift_slab", i32, _vp, u32, _vp)

@@ -144,6 +144,11 @@ class PmcContext:
         """Strong-scaling start: the whole box's lattice, this slab's planes (pmc_init_lattice_global)."""
         check("pmc_init_lattice_global", lib().pmc_init_lattice_global(self._h, n_atoms_total))
 
+    def init_lattice_planes(self, n_atoms_lattice: int, lattice_cps_z: int) -> None:
+        """The lattice of a taller box (cps x cps x lattice_cps_z cells), bottom-aligned; this slab's
+        planes of it (pmc_init_lattice_planes; the config-5 weak-scaling start)."""
+        check("pmc_init_lattice_planes", lib().pmc_init_lattice_planes(self._h, n_atoms_lattice, lattice_cps_z))
+
     def sweep(self, s: int) -> None:
         check("pmc_sweep", lib().pmc_sweep(self._h, s))
 
@@ -187,6 +192,14 @@ class PmcContext:
         """Summed kernel durations (dispatch-packet HIP events) of the subsweep / shift launches
         since the last call; then per-launch timing on or off (pmc_timing)."""
         return self._timing("pmc_timing", enable)
+
+    def timing_kinds(self, enable: bool) -> dict:
+        """Per-kind kernel durations (pmc_timing_kinds): context-stream subsweep launches, shift
+        launches, other-stream (slab boundary) subsweep launches."""
+        ms, cnt = (C.c_double * 3)(), (C.c_int * 3)()
+        check("pmc_timing_kinds", lib().pmc_timing_kinds(self._h, int(enable), C.byref(ms), C.byref(cnt)))
+        return {"subsweep_ms": ms[0], "n_subsweep": cnt[0], "shift_ms": ms[1], "n_shift": cnt[1],
+                "boundary_ms": ms[2], "n_boundary": cnt[2]}
 
     def slab_timing(self, enable: bool) -> dict:
         return self._timing("pmc_slab_timing", enable)
