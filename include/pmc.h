@@ -51,9 +51,13 @@ typedef struct pmc_params {
     float w;            /* cell width == LJ cutoff rc (w); box L = cps * w */
     float beta;         /* inverse temperature (beta) */
     float sigma;        /* Gaussian trial-move width (sigma) */
-    uint32_t reserved;
+    uint32_t flags;     /* PMC_FLAG_*: 0 = defaults */
     uint64_t seed;      /* Philox key; the reference seeds cuRAND with 1234 (subsweep.h:259) */
 } pmc_params;
+/* pmc_params.flags: colour order of a sweep.  Default (0): grouped by z parity (4 colours of one
+ * parity, then the other 4; spec v9, pmc_detmath.h); PMC_FLAG_FULL_SHUFFLE: one shuffle of all 8
+ * colours (the reference's FY_Shuffle, start.cu:34-44). */
+#define PMC_FLAG_FULL_SHUFFLE 1u
 
 /* Observables accumulated by the subsweep kernels (reference: kernel.cu:228,413-415 --
  * accept_counter and d_Eblocks; the reference never reports acceptance). */
@@ -210,8 +214,13 @@ int pmc_slab_timing(pmc_ctx* ctx, int enable, double* subsweep_ms, int* n_subswe
  * start.cu:34-44,153-157, reseeded from time() in the reference) and the shift axis/distance
  * (kernel.cu:683-684), all from the host Philox stream keyed by `seed`. */
 int pmc_sweep_plan(uint64_t seed, uint32_t sweep, float w, int order[8], int* f, float* d);
+int pmc_sweep_plan_ex(uint64_t seed, uint32_t sweep, float w, uint32_t flags, int order[8], int* f, float* d);
 /* mc_passes sweeps starting at sweep index `first_sweep` (the `start` driver). */
 int pmc_start(pmc_ctx* ctx, uint32_t first_sweep, int mc_passes, pmc_result* out);
+/* pmc_start with flags: PMC_START_NO_ENERGY skips the two cell-list energies (e_initial/e_final
+ * are NaN), for drivers that evaluate the energy once per interval themselves. */
+#define PMC_START_NO_ENERGY 1
+int pmc_start_ex(pmc_ctx* ctx, uint32_t first_sweep, int mc_passes, int flags, pmc_result* out);
 /* Record the sweep loop (pmc_sweep for sweeps first..first+count-1) as a hipGraph and
  * replay it; identical results to calling pmc_sweep in a loop. */
 int pmc_run_graph(pmc_ctx* ctx, uint32_t first_sweep, int count);
@@ -270,6 +279,10 @@ int pmc_read_dump(const char* path, int64_t frame, int64_t* timestep, float* h_r
  * reads the header only). */
 int pmc_snapshot_write(const char* path, const pmc_params* params, uint32_t next_sweep,
                        const pmc_stats* stats, const float* h_disk, const int16_t* h_n, int64_t cells);
+/* pmc_snapshot_read: with h_disk/h_n, params is required and params->nmax must be the nmax the
+ * buffers were sized for (cells*3*nmax floats): a snapshot with another nmax is refused before
+ * anything is written (PMC_ERR_ARG); on return *params holds the snapshot's parameters.  Header and
+ * payload come from one open file. */
 int pmc_snapshot_read(const char* path, pmc_params* params, uint32_t* next_sweep, pmc_stats* stats,
                       float* h_disk, int16_t* h_n, int64_t cells);
 /* Context wrappers (owned cells; slab mode: this rank's planes, halos must be exchanged after a

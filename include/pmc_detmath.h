@@ -261,6 +261,29 @@ PMC_HD int64_t pmc_to_fixed(double e) {
     return r;
 }
 
+/* pmc_to_fixed((double)f) for a float f, in integer arithmetic only (no f64 ops: the GPU energy
+ * kernel converts every pair term): f = m * 2^(ex-150), so f * 2^32 = m * 2^(ex-118); exact left
+ * shift, or a right shift rounding half away from zero (the magnitude rounds, the sign is
+ * reapplied: pmc_to_fixed is symmetric).  |f| > 2^30 clamps to +-2^62 as pmc_to_fixed does;
+ * zeros and subnormals (< 2^-126, so |f * 2^32| < 0.5) give 0.  Finite f only. */
+PMC_HD int64_t pmc_to_fixed_f32(float f) {
+    /* branch-free (selects only): the GPU kernel converts a 64-lane block of terms at once */
+    const uint32_t b = pmc_fbits(f);
+    const uint32_t ex = (b >> 23) & 0xFFu;
+    const uint32_t man = b & 0x7FFFFFu;
+    const uint32_t m = man | 0x800000u;            /* ex == 0 (zero/subnormal) rounds to 0 below */
+    const int sh = (int)ex - 118;
+    const int sl = sh < 0 ? 0 : (sh > 39 ? 39 : sh);
+    const int sr = sh >= 0 ? 1 : (-sh > 25 ? 25 : -sh);
+    const uint64_t left = (uint64_t)m << sl;
+    /* magnitude m * 2^-sr rounded half away from zero = floor(m / 2^sr + 1/2); m < 2^24, so
+     * sr = 25 gives 0 for every smaller exponent too */
+    const uint64_t right = (uint64_t)((m + (1u << (sr - 1))) >> sr);
+    uint64_t q = sh >= 0 ? left : right;
+    q = (ex > 157u || (ex == 157u && man != 0u)) ? ((uint64_t)1 << 62) : q;
+    return (b >> 31) ? -(int64_t)q : (int64_t)q;
+}
+
 /* ------------------------------------------------------------------------------------- */
 /* Sweep plan: colour order + shift (f, d), replicated on every rank (no broadcast).      */
 /* Reference: FY_Shuffle + itoa (start.cu:34-44,153-157), f/d (kernel.cu:683-684).        */
@@ -278,23 +301,50 @@ PMC_HD void pmc_colour_offset(int colour, int off[3]) {
     off[0] = (colour / 4) % 2;
 }
 
-PMC_HD pmc_sweep_plan_t pmc_plan_for_sweep(uint64_t seed, uint32_t sweep, float w) {
+/* Colour order (spec v9).  Default: grouped by z parity -- the 4 colours of one z parity
+ * (offset[2] = colour % 2, itoa start.cu:153-157), then the 4 of the other; which parity goes
+ * first from word 0, each group Fisher-Yates-shuffled (words 1-3 and 4-6).  Every colour phase is
+ * a Metropolis update that preserves the Boltzmann distribution, so any order is a valid sweep;
+ * this one lets a z-slab decomposition exchange halos twice per sweep instead of up to 8 times
+ * ("colour grouping by z-parity").  PMC_PLAN_FULL_SHUFFLE: one Fisher-Yates over all 8
+ * (the reference's FY_Shuffle, start.cu:34-44, made standard and Philox-driven). */
+#define PMC_PLAN_FULL_SHUFFLE 1u
+PMC_HD pmc_sweep_plan_t pmc_plan_for_sweep_ex(uint64_t seed, uint32_t sweep, float w, uint32_t flags) {
     uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
     pmc_u32x4 a = pmc_philox4x32_10(0u, 0xFFFFFFFFu, sweep, PMC_TAG_PLAN, k0, k1);
     pmc_u32x4 b = pmc_philox4x32_10(1u, 0xFFFFFFFFu, sweep, PMC_TAG_PLAN, k0, k1);
     uint32_t words[8] = {a.v[0], a.v[1], a.v[2], a.v[3], b.v[0], b.v[1], b.v[2], b.v[3]};
     pmc_sweep_plan_t p;
-    for (int i = 0; i < 8; ++i) p.order[i] = i;
-    /* standard Fisher-Yates (fixes D1: the reference swaps a[n-i] and reseeds from time()) */
-    for (int i = 7; i > 0; --i) {
-        uint32_t j = pmc_bounded(words[7 - i], (uint32_t)(i + 1));
-        int t = p.order[i]; p.order[i] = p.order[j]; p.order[j] = t;
+    if (flags & PMC_PLAN_FULL_SHUFFLE) {
+        for (int i = 0; i < 8; ++i) p.order[i] = i;
+        /* standard Fisher-Yates (fixes D1: the reference swaps a[n-i] and reseeds from time()) */
+        for (int i = 7; i > 0; --i) {
+            uint32_t j = pmc_bounded(words[7 - i], (uint32_t)(i + 1));
+            int t = p.order[i]; p.order[i] = p.order[j]; p.order[j] = t;
+        }
+    } else {
+        const int p0 = (int)pmc_bounded(words[0], 2u);
+        for (int i = 0; i < 4; ++i) {
+            p.order[i] = 2 * i + p0;
+            p.order[4 + i] = 2 * i + (1 - p0);
+        }
+        for (int i = 3; i > 0; --i) {
+            uint32_t j = pmc_bounded(words[4 - i], (uint32_t)(i + 1));        /* words 1..3 */
+            int t = p.order[i]; p.order[i] = p.order[j]; p.order[j] = t;
+        }
+        for (int i = 3; i > 0; --i) {
+            uint32_t j = pmc_bounded(words[7 - i], (uint32_t)(i + 1));        /* words 4..6 */
+            int t = p.order[4 + i]; p.order[4 + i] = p.order[4 + j]; p.order[4 + j] = t;
+        }
     }
     p.f = (int)pmc_bounded(words[7], 3u);
     pmc_u32x4 c = pmc_philox4x32_10(2u, 0xFFFFFFFFu, sweep, PMC_TAG_PLAN, k0, k1);
     float u = pmc_u01(c.v[0]);
     p.d = u * w - w / 2.0f;
     return p;
+}
+PMC_HD pmc_sweep_plan_t pmc_plan_for_sweep(uint64_t seed, uint32_t sweep, float w) {
+    return pmc_plan_for_sweep_ex(seed, sweep, w, 0u);
 }
 
 /* ------------------------------------------------------------------------------------- */

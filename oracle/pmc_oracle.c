@@ -34,6 +34,7 @@ int orc_params_check(pmc_params* p) {
     if ((p->cps_x | p->cps_y | p->cps_z | p->nz_local | p->z0) & 1) return PMC_ERR_ARG;
     if (p->nmax < 1 || p->nmax > 64 || p->n_moves < 0) return PMC_ERR_ARG;
     if (p->halo != 0 && p->halo != 1) return PMC_ERR_ARG;
+    if (p->flags & ~PMC_FLAG_FULL_SHUFFLE) return PMC_ERR_ARG;
     if (!p->halo && (p->nz_local != p->cps_z || p->z0 != 0)) return PMC_ERR_ARG;
     if (p->z0 < 0 || p->z0 + p->nz_local > p->cps_z) return PMC_ERR_ARG;
     return PMC_OK;
@@ -449,7 +450,7 @@ int orc_run(const pmc_params* p, float* disk, int16_t* n, float* sdisk, int16_t*
     int over = 0;
     for (int k = 0; k < nsweeps; ++k) {
         uint32_t s = first + (uint32_t)k;
-        pmc_sweep_plan_t plan = pmc_plan_for_sweep(p->seed, s, p->w);
+        pmc_sweep_plan_t plan = pmc_plan_for_sweep_ex(p->seed, s, p->w, p->flags);
         for (int c = 0; c < 8; ++c) {
             int o[3];
             pmc_colour_offset(plan.order[c], o);
@@ -481,9 +482,14 @@ float orc_pair_energy(float dx, float dy, float dz, float rc2) {
     return pmc_lj_from_r2(pmc_r2(dx, dy, dz), rc2);
 }
 void orc_sweep_plan(uint64_t seed, uint32_t sweep, float w, int order[8], int* f, float* d) {
-    pmc_sweep_plan_t pl = pmc_plan_for_sweep(seed, sweep, w);
+    orc_sweep_plan_ex(seed, sweep, w, 0u, order, f, d);
+}
+
+void orc_sweep_plan_ex(uint64_t seed, uint32_t sweep, float w, uint32_t flags, int order[8], int* f, float* d) {
+    pmc_sweep_plan_t pl = pmc_plan_for_sweep_ex(seed, sweep, w, flags);
     for (int i = 0; i < 8; ++i) order[i] = pl.order[i];
     *f = pl.f;
     *d = pl.d;
 }
 int64_t orc_to_fixed(double e) { return pmc_to_fixed(e); }
+int64_t orc_to_fixed_f32(float f) { return pmc_to_fixed_f32(f); }

@@ -59,7 +59,9 @@ void orc_det_sincos_2pi(float u, float* s, float* c);
 void orc_move_normals(const uint32_t w[4], float g[3]);
 float orc_pair_energy(float dx, float dy, float dz, float rc2);
 void orc_sweep_plan(uint64_t seed, uint32_t sweep, float w, int order[8], int* f, float* d);
+void orc_sweep_plan_ex(uint64_t seed, uint32_t sweep, float w, uint32_t flags, int order[8], int* f, float* d);
 int64_t orc_to_fixed(double e);
+int64_t orc_to_fixed_f32(float f);
 
 #ifdef __cplusplus
 }

@@ -25,7 +25,7 @@ class Params(C.Structure):
         ("nz_local", C.c_int32), ("z0", C.c_int32), ("halo", C.c_int32),
         ("nmax", C.c_int32), ("n_moves", C.c_int32),
         ("w", C.c_float), ("beta", C.c_float), ("sigma", C.c_float),
-        ("reserved", C.c_uint32), ("seed", C.c_uint64),
+        ("flags", C.c_uint32), ("seed", C.c_uint64),
     ]
 
 
@@ -38,8 +38,8 @@ class Stats(C.Structure):
 
 
 def make_params(cps=4, cps_y=0, cps_z=0, nz_local=0, z0=0, halo=0, nmax=16, n_moves=10,
-                w=2.5, beta=0.3, sigma=0.5, seed=1234) -> Params:
-    p = Params(cps, cps_y, cps_z, nz_local, z0, halo, nmax, n_moves, w, beta, sigma, 0, seed)
+                w=2.5, beta=0.3, sigma=0.5, seed=1234, flags=0) -> Params:
+    p = Params(cps, cps_y, cps_z, nz_local, z0, halo, nmax, n_moves, w, beta, sigma, flags, seed)
     return p
 
 
@@ -96,8 +96,13 @@ def lib():
         L.orc_sweep_plan.argtypes = [C.c_uint64, C.c_uint32, C.c_float, C.POINTER(C.c_int * 8),
                                      C.POINTER(C.c_int), C.POINTER(C.c_float)]
         L.orc_sweep_plan.restype = None
+        L.orc_sweep_plan_ex.argtypes = [C.c_uint64, C.c_uint32, C.c_float, C.c_uint32, C.POINTER(C.c_int * 8),
+                                        C.POINTER(C.c_int), C.POINTER(C.c_float)]
+        L.orc_sweep_plan_ex.restype = None
         L.orc_to_fixed.argtypes = [C.c_double]
         L.orc_to_fixed.restype = C.c_int64
+        L.orc_to_fixed_f32.argtypes = [C.c_float]
+        L.orc_to_fixed_f32.restype = C.c_int64
         _lib = L
     return _lib
 
@@ -212,11 +217,11 @@ def det_sincos_2pi(u: float):
     return s.value, c.value
 
 
-def sweep_plan(seed: int, sweep: int, w: float = 2.5):
+def sweep_plan(seed: int, sweep: int, w: float = 2.5, flags: int = 0):
     order = (C.c_int * 8)()
     f = C.c_int()
     d = C.c_float()
-    lib().orc_sweep_plan(seed, sweep, w, C.byref(order), C.byref(f), C.byref(d))
+    lib().orc_sweep_plan_ex(seed, sweep, w, flags, C.byref(order), C.byref(f), C.byref(d))
     return list(order), f.value, d.value
 
 

@@ -83,6 +83,7 @@ int normalise(pmc_params* p) {
     if (p->nmax < 1 || p->nmax > 64) return fail(PMC_ERR_ARG, "nmax must be in 1..64");
     if (p->n_moves < 0) return fail(PMC_ERR_ARG, "n_moves must be >= 0");
     if (p->halo != 0 && p->halo != 1) return fail(PMC_ERR_ARG, "halo must be 0 or 1");
+    if (p->flags & ~PMC_FLAG_FULL_SHUFFLE) return fail(PMC_ERR_ARG, "unknown flags");
     if (!p->halo && (p->nz_local != p->cps_z || p->z0 != 0))
         return fail(PMC_ERR_ARG, "halo == 0 requires the whole box (nz_local == cps_z, z0 == 0)");
     if (p->z0 < 0 || p->z0 + p->nz_local > p->cps_z) return fail(PMC_ERR_ARG, "slab outside the box");
@@ -110,6 +111,8 @@ DevGeom make_geom(const pmc_params& p) {
     g.r2min = PMC_R2_MIN;
     g.div_ncx = make_udiv_magic((uint32_t)(p.cps_x / 2));
     g.div_ncy = make_udiv_magic((uint32_t)(p.cps_y / 2));
+    g.div_cx = make_udiv_magic((uint32_t)p.cps_x);
+    g.div_plane = make_udiv_magic((uint32_t)p.cps_x * (uint32_t)p.cps_y);
     g.k0 = (uint32_t)p.seed;
     g.k1 = (uint32_t)(p.seed >> 32);
     for (int r = 0; r < 10; ++r) {
@@ -166,7 +169,7 @@ const LaunchTiming* next_timing(pmc_ctx* c, int kind, LaunchTiming* lt) {
 }
 
 int enqueue_sweep(pmc_ctx* c, uint32_t sweep) {
-    const pmc_sweep_plan_t plan = pmc_plan_for_sweep(c->P.seed, sweep, c->P.w);
+    const pmc_sweep_plan_t plan = pmc_plan_for_sweep_ex(c->P.seed, sweep, c->P.w, c->P.flags);
     for (int k = 0; k < 8; ++k) {
         int o[3];
         pmc_colour_offset(plan.order[k], o);
@@ -361,8 +364,13 @@ int pmc_shift_cells(pmc_ctx* c, const float* din, const int16_t* nin, float* dou
 }
 
 int pmc_sweep_plan(uint64_t seed, uint32_t sweep, float w, int order[8], int* f, float* d) {
+    return pmc_sweep_plan_ex(seed, sweep, w, 0u, order, f, d);
+}
+
+int pmc_sweep_plan_ex(uint64_t seed, uint32_t sweep, float w, uint32_t flags, int order[8], int* f, float* d) {
     if (!order || !f || !d) return fail(PMC_ERR_ARG, "null argument");
-    const pmc_sweep_plan_t plan = pmc_plan_for_sweep(seed, sweep, w);
+    if (flags & ~PMC_FLAG_FULL_SHUFFLE) return fail(PMC_ERR_ARG, "unknown plan flags");
+    const pmc_sweep_plan_t plan = pmc_plan_for_sweep_ex(seed, sweep, w, flags);
     for (int k = 0; k < 8; ++k) order[k] = plan.order[k];
     *f = plan.f;
     *d = plan.d;
@@ -457,7 +465,7 @@ int pmc_phase(pmc_ctx* c, int colour, uint32_t sweep) {
 
 int pmc_shift(pmc_ctx* c, uint32_t sweep) {
     if (!c) return fail(PMC_ERR_ARG, "null ctx");
-    const pmc_sweep_plan_t plan = pmc_plan_for_sweep(c->P.seed, sweep, c->P.w);
+    const pmc_sweep_plan_t plan = pmc_plan_for_sweep_ex(c->P.seed, sweep, c->P.w, c->P.flags);
     int rc = pmc_shift_cells(c, c->disk[c->cur], c->n[c->cur], c->disk[c->cur ^ 1], c->n[c->cur ^ 1], plan.f,
                              plan.d);
     if (rc) return rc;
@@ -468,7 +476,7 @@ int pmc_shift(pmc_ctx* c, uint32_t sweep) {
 int pmc_shift_slab(pmc_ctx* c, uint32_t sweep, int* halo_recv) {
     if (!c || !halo_recv) return fail(PMC_ERR_ARG, "null argument");
     if (!c->P.halo) return fail(PMC_ERR_ARG, "pmc_shift_slab needs a slab context (halo = 1)");
-    const pmc_sweep_plan_t plan = pmc_plan_for_sweep(c->P.seed, sweep, c->P.w);
+    const pmc_sweep_plan_t plan = pmc_plan_for_sweep_ex(c->P.seed, sweep, c->P.w, c->P.flags);
     int zl0, zl1;
     *halo_recv = slab_shift_planes(c->P.nz_local, plan, &zl0, &zl1);
     LaunchTiming lt;
@@ -560,16 +568,17 @@ int pmc_error_flags(pmc_ctx* c, uint32_t* flags, int reset) {
     return PMC_OK;
 }
 
-int pmc_start(pmc_ctx* c, uint32_t first, int mc_passes, pmc_result* out) {
+int pmc_start_ex(pmc_ctx* c, uint32_t first, int mc_passes, int flags, pmc_result* out) {
     if (!c || mc_passes < 0) return fail(PMC_ERR_ARG, "bad argument");
     if (c->P.halo) return fail(PMC_ERR_ARG, "pmc_start drives the whole box; use the slab driver for halo mode");
+    const bool energies = !(flags & PMC_START_NO_ENERGY);
     pmc_result r;
     std::memset(&r, 0, sizeof(r));
+    r.e_initial = r.e_final = std::nan("");
     pmc_stats s0;
     int rc = pmc_stats_read(c, &s0, 0);
     if (rc) return rc;
-    rc = pmc_energy(c, &r.e_initial);
-    if (rc) return rc;
+    if (energies && (rc = pmc_energy(c, &r.e_initial))) return rc;
     PMC_HIP(hipEventRecord(c->ev0, c->stream));
     for (int k = 0; k < mc_passes; ++k) {
         rc = enqueue_sweep(c, first + (uint32_t)k);
@@ -580,8 +589,7 @@ int pmc_start(pmc_ctx* c, uint32_t first, int mc_passes, pmc_result* out) {
     float ms = 0.0f;
     PMC_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));
     r.seconds = ms * 1e-3;
-    rc = pmc_energy(c, &r.e_final);
-    if (rc) return rc;
+    if (energies && (rc = pmc_energy(c, &r.e_final))) return rc;
     pmc_stats s1;
     rc = pmc_stats_read(c, &s1, 0);
     if (rc) return rc;
@@ -596,6 +604,10 @@ int pmc_start(pmc_ctx* c, uint32_t first, int mc_passes, pmc_result* out) {
     if (out) *out = r;
     if (fl & 1u) return fail(PMC_ERR_OVERFLOW, "shiftCells: cell occupancy exceeded nmax");
     return PMC_OK;
+}
+
+int pmc_start(pmc_ctx* c, uint32_t first, int mc_passes, pmc_result* out) {
+    return pmc_start_ex(c, first, mc_passes, 0, out);
 }
 
 int pmc_copy_out(pmc_ctx* c, float* h_disk, int16_t* h_n) {
@@ -722,23 +734,25 @@ int pmc_save_snapshot(pmc_ctx* c, const char* path, uint32_t next_sweep) {
 
 int pmc_load_snapshot(pmc_ctx* c, const char* path, uint32_t* next_sweep) {
     if (!c || !path) return fail(PMC_ERR_ARG, "bad argument");
-    pmc_params q;
-    uint32_t sw = 0;
-    pmc_stats st;
-    int rc = pmc_snapshot_read(path, &q, &sw, &st, nullptr, nullptr, 0);
-    if (rc) return rc;
     const pmc_params& p = c->P;
-    if (q.cps_x != p.cps_x || q.cps_y != p.cps_y || q.cps_z != p.cps_z || q.nz_local != p.nz_local || q.z0 != p.z0 ||
-        q.halo != p.halo || q.nmax != p.nmax || q.n_moves != p.n_moves || q.w != p.w || q.beta != p.beta ||
-        q.sigma != p.sigma || q.seed != p.seed)
-        return fail(PMC_ERR_ARG, "pmc_load_snapshot: snapshot parameters differ from the context's");
     int64_t first, count;
     owned_range(c, &first, &count);
     std::vector<float> disk((size_t)c->cells * 3 * (size_t)p.nmax, 0.0f);
     std::vector<int16_t> n((size_t)c->cells, 0);
-    if ((rc = pmc_snapshot_read(path, nullptr, nullptr, nullptr, disk.data() + (size_t)first * 3 * (size_t)p.nmax,
-                                n.data() + first, count)))
-        return rc;
+    // one open file: header and payload; the reader rejects an nmax other than ours before
+    // writing into the buffers (sized for our nmax)
+    pmc_params q;
+    std::memset(&q, 0, sizeof(q));
+    q.nmax = p.nmax;
+    uint32_t sw = 0;
+    pmc_stats st;
+    int rc = pmc_snapshot_read(path, &q, &sw, &st, disk.data() + (size_t)first * 3 * (size_t)p.nmax,
+                               n.data() + first, count);
+    if (rc) return rc;
+    if (q.cps_x != p.cps_x || q.cps_y != p.cps_y || q.cps_z != p.cps_z || q.nz_local != p.nz_local || q.z0 != p.z0 ||
+        q.halo != p.halo || q.nmax != p.nmax || q.n_moves != p.n_moves || q.w != p.w || q.beta != p.beta ||
+        q.sigma != p.sigma || q.seed != p.seed || q.flags != p.flags)
+        return fail(PMC_ERR_ARG, "pmc_load_snapshot: snapshot parameters differ from the context's");
     if ((rc = pmc_copy_in(c, disk.data(), n.data()))) return rc;   // halo planes: zero until exchanged
     if ((rc = pmc_stats_write(c, &st))) return rc;
     if (next_sweep) *next_sweep = sw;
@@ -876,12 +890,12 @@ struct pmc_slab {
     int rank = 0, world = 1, below = 0, above = 0;
     ncclComm_t comm = nullptr;            // RCCL transport
     pmc_local_group* group = nullptr;     // in-process transport (not owned)
-    hipStream_t aux = nullptr;            // boundary planes + exchanges ("T")
+    hipStream_t aux = nullptr;            // halo exchanges ("T")
+    hipStream_t hi = nullptr;             // the upper plane chain (two-chain schedule)
+    int chains = 1;                       // plane chains (streams running subsweeps): 1 or 2
     hipEvent_t ev_i = nullptr, ev_b = nullptr, ev_t = nullptr;
-    float* sbuf = nullptr;                // packed colour cells of the sent plane
-    float* rbuf = nullptr;                // ... of the received plane
-    size_t pack_floats = 0;
-    int pend_colour = -1, pend_dst = 0;   // unpack owed on aux (colour, halo plane)
+    hipEvent_t ev_x = nullptr;            // T after its latest exchange
+    hipEvent_t ev_run[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};   // [chain][parity] run ends
     std::vector<XferMsg> sends, recvs;    // the exchange being assembled
     bool messages() const { return comm != nullptr || group != nullptr; }
 };
@@ -898,10 +912,11 @@ void drop_slab(pmc_ctx* c) {
         s->group->slot[s->rank].joined = false;
     }
     if (s->aux) (void)hipStreamDestroy(s->aux);
-    for (hipEvent_t e : {s->ev_i, s->ev_b, s->ev_t})
+    if (s->hi) (void)hipStreamSynchronize(s->hi);
+    for (hipEvent_t e : {s->ev_i, s->ev_b, s->ev_t, s->ev_x, s->ev_run[0][0], s->ev_run[0][1], s->ev_run[1][0],
+                         s->ev_run[1][1]})
         if (e) (void)hipEventDestroy(e);
-    if (s->sbuf) (void)hipFree(s->sbuf);
-    if (s->rbuf) (void)hipFree(s->rbuf);
+    if (s->hi) (void)hipStreamDestroy(s->hi);
     delete s;
     c->slab = nullptr;
 }
@@ -993,32 +1008,27 @@ float* disk_plane(pmc_ctx* c, int z) { return c->disk[c->cur] + (size_t)(z + 1) 
 int16_t* n_plane(pmc_ctx* c, int z) { return c->n[c->cur] + (size_t)(z + 1) * plane_cells(c); }
 
 
-// finish the previous phase exchange on aux: unpack the received colour cells into the halo
-int slab_complete(pmc_ctx* c) {
+// End of a run of colour phases of z parity p (spec v9 groups the 8 phases of a sweep into two
+// runs): during the run only the owned planes of parity p changed, and the one of them another rank
+// holds as a halo is the boundary plane P_p (plane 0 for p = 0, nz-1 for p = 1).  It goes whole
+// (every colour of the run touched it; counts do not change in a subsweep) to the neighbour that
+// holds it -- the rank below for p = 0, above for p = 1 -- and the matching halo H_p (top for p = 0,
+// bottom for p = 1) comes from the other side: one message each way, straight from and into the
+// state buffer (no packing).  The next run (parity 1-p) is the first to read H_p.  A single rank
+// without messages copies its own plane into its periodic halo.  On aux.
+int slab_exchange_run(pmc_ctx* c, int p) {
     pmc_slab* s = c->slab;
-    if (s->pend_colour < 0) return PMC_OK;
-    hipError_t e = launch_colour_rows(c->G, s->rbuf, disk_plane(c, s->pend_dst), s->pend_colour, 1, s->aux);
-    s->pend_colour = -1;
-    return e == hipSuccess ? PMC_OK : hip_fail(e, "unpack launch");
-}
-
-// after colour phase `colour`: its boundary plane (z-parity oz = colour % 2, start.cu:153-157)
-// goes to the neighbour that holds it as a halo; the matching halo comes from the other side.
-// Only that colour's quarter of the plane changed, so only it travels: the boundary launch wrote
-// those rows packed into sbuf (mirror rows); the received ones are unpacked by slab_complete.
-// A single rank needs nothing here: its boundary launch mirrored the rows into its own halo.
-int slab_exchange_phase(pmc_ctx* c, int colour) {
-    pmc_slab* s = c->slab;
-    if (!s->messages()) return PMC_OK;
-    const bool down = colour % 2 == 0;                 // oz = 0: plane 0 -> below, top halo <- above
-    const int to = down ? s->below : s->above, from = down ? s->above : s->below;
-    xfer_send(s, s->sbuf, s->pack_floats * 4, to);
-    xfer_recv(s, s->rbuf, s->pack_floats * 4, from);
-    int rc = xfer_run(s);
-    if (rc) return rc;
-    s->pend_colour = colour;
-    s->pend_dst = down ? c->P.nz_local : -1;
-    return PMC_OK;
+    const int nz = c->P.nz_local;
+    const size_t pf = plane_floats(c);
+    const int src = p == 0 ? 0 : nz - 1, dst = p == 0 ? nz : -1;
+    if (!s->messages()) {
+        PMC_HIP(hipMemcpyAsync(disk_plane(c, dst), disk_plane(c, src), pf * 4, hipMemcpyDeviceToDevice, s->aux));
+        return PMC_OK;
+    }
+    const int to = p == 0 ? s->below : s->above, from = p == 0 ? s->above : s->below;
+    xfer_send(s, disk_plane(c, src), pf * 4, to);
+    xfer_recv(s, disk_plane(c, dst), pf * 4, from);
+    return xfer_run(s);
 }
 
 // both boundary planes with their counts (after shiftCells / initialisation), on aux
@@ -1104,25 +1114,38 @@ int slab_attach(pmc_ctx* c, int rank, int world, bool messages) {
         drop_slab(c);
         return hip_fail(e, "hipStreamCreate");
     }
-    for (hipEvent_t* ev : {&s->ev_i, &s->ev_b, &s->ev_t})
+    for (hipEvent_t* ev : {&s->ev_i, &s->ev_b, &s->ev_t, &s->ev_x, &s->ev_run[0][0], &s->ev_run[0][1],
+                           &s->ev_run[1][0], &s->ev_run[1][1]})
         if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) {
             drop_slab(c);
             return hip_fail(e, "hipEventCreate");
         }
-    s->pack_floats = (size_t)(c->P.cps_x / 2) * (c->P.cps_y / 2) * 3 * c->P.nmax;
+    // Two plane chains (lower and upper half of the slab on two streams) when the halves keep the
+    // checkerboard parity (nz % 4 == 0); PMC_SLAB_CHAINS=1 forces one.
+    {
+        static const int forced = [] {
+            const char* v = std::getenv("PMC_SLAB_CHAINS");
+            return v ? std::atoi(v) : 0;
+        }();
+        s->chains = (c->P.nz_local % 4 == 0 && forced != 1) ? 2 : 1;
+    }
+    if (s->chains == 2 && (e = hipStreamCreateWithFlags(&s->hi, hipStreamNonBlocking)) != hipSuccess) {
+        drop_slab(c);
+        return hip_fail(e, "hipStreamCreate");
+    }
+    // every "latest" event starts recorded (waits on them are no-ops until real work records them)
+    for (hipEvent_t ev : {s->ev_x, s->ev_run[0][0], s->ev_run[0][1], s->ev_run[1][0], s->ev_run[1][1]})
+        if ((e = hipEventRecord(ev, c->stream)) != hipSuccess) {
+            drop_slab(c);
+            return hip_fail(e, "hipEventRecord");
+        }
     if (!c->ovf_aux) {   // the boundary launches' overflow queue (they run beside the interior's)
         if ((e = hipMalloc(&c->ovf_aux, c->ovf_bytes)) != hipSuccess || (e = hipMemset(c->ovf_aux, 0, c->ovf_bytes)) != hipSuccess) {
             drop_slab(c);
             return hip_fail(e, "hipMalloc overflow queue");
         }
     }
-    if (messages) {
-        if ((e = hipMalloc(&s->sbuf, s->pack_floats * 4)) != hipSuccess ||
-            (e = hipMalloc(&s->rbuf, s->pack_floats * 4)) != hipSuccess) {
-            drop_slab(c);
-            return hip_fail(e, "hipMalloc halo buffers");
-        }
-    }
+    (void)messages;   // halo messages go straight from and into the state buffers
     return PMC_OK;
 }
 
@@ -1196,10 +1219,10 @@ int pmc_slab_exchange(pmc_ctx* c) {
     pmc_slab* s = c->slab;
     PMC_HIP(hipEventRecord(s->ev_i, c->stream));
     PMC_HIP(hipStreamWaitEvent(s->aux, s->ev_i, 0));
-    int rc = slab_complete(c);
+    int rc = slab_exchange_full(c);
     if (rc) return rc;
-    if ((rc = slab_exchange_full(c))) return rc;
     PMC_HIP(hipEventRecord(s->ev_t, s->aux));
+    PMC_HIP(hipEventRecord(s->ev_x, s->aux));
     PMC_HIP(hipStreamWaitEvent(c->stream, s->ev_t, 0));
     return PMC_OK;
 }
@@ -1209,55 +1232,74 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
     pmc_slab* s = c->slab;
     hipStream_t S = c->stream, T = s->aux;
     const int nz = c->P.nz_local;
-    const pmc_sweep_plan_t plan = pmc_plan_for_sweep(c->P.seed, sweep, c->P.w);
+    const int m = s->chains;
+    hipStream_t chain[2] = {S, s->hi};
+    int* queue[2] = {c->ovf, c->ovf_aux};
+    const int zlo[2] = {0, m == 2 ? nz / 2 : nz}, zhi[2] = {m == 2 ? nz / 2 : nz, nz};
+    const pmc_sweep_plan_t plan = pmc_plan_for_sweep_ex(c->P.seed, sweep, c->P.w, c->P.flags);
     hipError_t e;
     int rc;
-    // Per colour k:  S: wait B(k-1) -> interior I(k) = planes [1, nz-1) (reads no halo)
-    //                T: wait I(k-1) -> boundary B(k) = the one boundary plane of parity oz ->
-    //                   RCCL send/recv of its colour cells (packed by B(k)) -> unpack into the halo.
-    // I(k) and B(k) run together; exchange k overlaps I(k+1).  I(k) never writes a plane an
-    // exchange reads, nor reads a halo one writes.  Cells of a colour are independent, so any
-    // split of a phase gives the whole-box result bit for bit.
-    // The cross-stream waits are only needed when the z parity changes: a phase of parity p
-    // writes planes of parity p and reads its own plane and the planes of parity 1-p, so I(k) and
-    // B(k-1) (or B(k) and I(k-1)) of equal parity touch disjoint planes.  The wait at the start of
-    // a run of equal parities orders it after every earlier phase of the other parity.
-    PMC_HIP(hipEventRecord(s->ev_i, S));                       // "I(-1)": all earlier S work
-    int prev_oz = -1;
-    for (int k = 0; k < 8; ++k) {
-        const int colour = plan.order[k];
-        int o[3];
-        pmc_colour_offset(colour, o);
-        if (o[2] != prev_oz) {
-            PMC_HIP(hipStreamWaitEvent(T, s->ev_i, 0));            // I(k-1)
-            if (k > 0) PMC_HIP(hipStreamWaitEvent(S, s->ev_b, 0)); // B(k-1)
+    // The 8 colour phases form runs of equal z parity q (two runs of 4 with the default plan).  In a
+    // run only the planes of parity q change, each reading its own plane and the parity 1-q planes
+    // next to it, which no phase of the run writes and no halo of the run changes: every plane's
+    // chain of phases is independent of the other planes' for the whole run.  So the slab's planes
+    // are split into m = 2 chains (lower half [0, nz/2) on the context stream, upper half on a
+    // second stream) that run each run's phases without any synchronisation between them -- one
+    // chain's launch gaps and tails overlap the other's work -- and synchronise only where a run's
+    // reads cross the split or a halo:
+    //   * a parity-1 run on the lower chain reads plane nz/2 (upper chain), a parity-0 run on the
+    //     upper chain reads plane nz/2-1 (lower chain): they wait for the other chain's previous run;
+    //   * at the end of a run of parity q the boundary plane P_q (plane 0 for q = 0, nz-1 for q = 1,
+    //     written by the lower resp. upper chain) goes whole to the neighbour rank holding it as a halo
+    //     and the matching halo H_q comes from the other side, on the exchange stream T
+    //     (slab_exchange_run), after the producing chain's run and the reading chain's previous run;
+    //   * the chain that reads H_q (the upper one for q = 0: top halo; the lower one for q = 1) waits
+    //     for that exchange before its next run.
+    // Cells of a colour are independent, so any split of a phase gives the whole-box result bit for
+    // bit (the GPU tests compare every world size with the oracle's whole box).
+    PMC_HIP(hipEventRecord(s->ev_i, S));                         // S after the previous sweep's shift
+    if (m == 2) PMC_HIP(hipStreamWaitEvent(chain[1], s->ev_i, 0));
+    int k = 0;
+    bool first_run = true;
+    while (k < 8) {
+        const int q = plan.order[k] % 2;                         // itoa: offset[2] = colour % 2
+        int k1 = k;
+        while (k1 < 8 && plan.order[k1] % 2 == q) ++k1;          // run [k, k1)
+        for (int j = 0; j < m; ++j) {
+            hipStream_t st = chain[j];
+            if (m == 2 && !first_run) {
+                if (q == 1 && j == 0) PMC_HIP(hipStreamWaitEvent(st, s->ev_run[1][0], 0));
+                if (q == 0 && j == 1) PMC_HIP(hipStreamWaitEvent(st, s->ev_run[0][1], 0));
+            }
+            // the halo this run reads (H_{1-q}: bottom for q = 0, top for q = 1) is received by T
+            const int halo_reader = q == 0 ? 0 : m - 1;
+            if (j == halo_reader) PMC_HIP(hipStreamWaitEvent(st, s->ev_x, 0));
+            for (int kk = k; kk < k1; ++kk) {
+                int o[3];
+                pmc_colour_offset(plan.order[kk], o);
+                LaunchTiming lt;
+                e = launch_subsweep(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep, c->stats, queue[j],
+                                    zlo[j], zhi[j], st, next_timing(c, j == 0 ? 0 : 2, &lt));
+                if (e != hipSuccess) return hip_fail(e, "subsweep launch");
+            }
+            PMC_HIP(hipEventRecord(s->ev_run[j][q], st));
         }
-        prev_oz = o[2];
-        if (nz > 2) {
-            LaunchTiming lt;
-            e = launch_subsweep(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep, c->stats, c->ovf, 1,
-                                nz - 1, S, next_timing(c, 0, &lt));
-            if (e != hipSuccess) return hip_fail(e, "subsweep launch");
-        }
-        PMC_HIP(hipEventRecord(s->ev_i, S));
-        // the boundary plane of this parity, full capacity (no fallback launch); its written-back
-        // rows go straight to the send buffer (RCCL) or to the periodic halo (single rank)
-        const bool down = o[2] == 0;
-        const int zb = down ? 0 : nz - 1;
-        float* mirror = s->messages() ? s->sbuf : disk_plane(c, down ? nz : -1);
-        LaunchTiming lt;
-        e = launch_subsweep_boundary(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep, c->stats, c->ovf_aux, zb,
-                                     zb + 1, mirror, s->messages() ? 0 : 1, T, next_timing(c, 2, &lt));
-        if (e != hipSuccess) return hip_fail(e, "subsweep launch");
-        PMC_HIP(hipEventRecord(s->ev_b, T));
-        // exchange k and its unpack follow B(k) on T straight away, so they run beside I(k)
-        // instead of between the wait for I(k) and B(k+1)
-        if ((rc = slab_exchange_phase(c, colour))) return rc;
-        if ((rc = slab_complete(c))) return rc;
+        // exchange of P_q / H_q: after the producing chain's run and the H_q reader's previous run
+        const int producer = q == 0 ? 0 : m - 1;
+        const int hq_reader = q == 0 ? m - 1 : 0;
+        PMC_HIP(hipStreamWaitEvent(T, s->ev_run[producer][q], 0));
+        PMC_HIP(hipStreamWaitEvent(T, s->ev_run[hq_reader][1 - q], 0));
+        if ((rc = slab_exchange_run(c, q))) return rc;
+        PMC_HIP(hipEventRecord(s->ev_x, T));
+        first_run = false;
+        k = k1;
     }
-    if ((rc = slab_complete(c))) return rc;
-    PMC_HIP(hipEventRecord(s->ev_t, T));
-    PMC_HIP(hipStreamWaitEvent(S, s->ev_t, 0));
+    // shiftCells reads every plane and both halos: join both chains and T
+    if (m == 2) {
+        PMC_HIP(hipEventRecord(s->ev_b, chain[1]));
+        PMC_HIP(hipStreamWaitEvent(S, s->ev_b, 0));
+    }
+    PMC_HIP(hipStreamWaitEvent(S, s->ev_x, 0));
     // shiftCells: after the 8 phases both halo planes are exact copies of the
     // neighbours' planes, so every halo plane whose new content depends only on planes this rank
     // holds is shifted here, bit-identical to its owner's result.  Along x or y that is both halo
@@ -1273,11 +1315,11 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
     c->cur ^= 1;
     // the next sweep's first boundary launch follows the shift on T ("I(-1)" wait); its first
     // interior reads no halo, so it overlaps the z exchange
-    if (dir != 0) {
-        PMC_HIP(hipEventRecord(s->ev_i, S));
-        PMC_HIP(hipStreamWaitEvent(T, s->ev_i, 0));
-        if ((rc = slab_exchange_zplane(c, dir))) return rc;
-    }
+    // T after the shift: the exchanges of the next sweep and the z halo read/write the new buffer
+    PMC_HIP(hipEventRecord(s->ev_i, S));
+    PMC_HIP(hipStreamWaitEvent(T, s->ev_i, 0));
+    if (dir != 0 && (rc = slab_exchange_zplane(c, dir))) return rc;
+    PMC_HIP(hipEventRecord(s->ev_x, T));
     PMC_HIP(hipEventRecord(s->ev_t, T));
     return PMC_OK;
 }

@@ -25,8 +25,8 @@ __host__ __device__ constexpr int subsweep_stride(int lcap) { return (lcap + 32 
 __host__ __device__ constexpr int lds_floats_per_wave(int lcap) { return 3 * subsweep_stride(lcap) + 2 * lcap + 64; }
 constexpr int kMainCap = 224;       // main launch: lds_floats_per_wave(224) * 4 B = 5120 B (32 waves/CU)
 static_assert(lds_floats_per_wave(kMainCap) * 4 <= 5120, "main-launch LDS per wave");
-constexpr int kStatCounters = 4;
-constexpr int kOvfHead = 2;       // ints of the subsweep overflow-queue header (pmc_kernels.hip)   // de_fixed, accepted, trials, evaluated
+constexpr int kStatCounters = 4;    // de_fixed, accepted, trials, evaluated
+constexpr int kOvfHead = 2;        // ints of the subsweep overflow-queue header (pmc_kernels.hip)
 
 // Unsigned division by an invariant d: n / d = (hi + ((n - hi) >> sh1)) >> sh2, hi = umulhi(n, mul)
 // (Granlund & Montgomery 1994, round-up variant; exact for every 32-bit n).
@@ -49,9 +49,10 @@ struct DevGeom {
     int nslot;                     // power of two >= nmax (lanes per cell in shift/energy)
     float w, beta, sigma, Lx, Ly, Lz, rc2;
     float rc2f;                    // staging filter threshold (pmc_filter_r2)
-    float r2min;
+    float r2min;                   // PMC_R2_MIN (passed as data so the kernel keeps it in an SGPR)
     UDivMagic div_ncx, div_ncy;    // division by cps_x/2 and cps_y/2 (subsweep cell decode)
-    uint32_t rk0[10], rk1[10];     // Philox round keys k + r*W (kernel arguments -> SGPRs, no key adds)                   // PMC_R2_MIN (passed as data so the kernel keeps it in an SGPR)
+    UDivMagic div_cx, div_plane;   // division by cps_x and cps_x*cps_y (energy cell decode)
+    uint32_t rk0[10], rk1[10];     // Philox round keys k + r*W (kernel arguments -> SGPRs, no key adds)
     uint32_t k0, k1;
 };
 

@@ -51,7 +51,7 @@ T get(const unsigned char* buf, size_t off) {
 // header field offsets (bytes)
 enum : size_t {
     H_MAGIC = 0, H_VERSION = 8, H_HBYTES = 12, H_INTS = 16 /* 8 x i32: cps_x..n_moves */,
-    H_W = 48, H_BETA = 52, H_SIGMA = 56, H_SEED = 64, H_SWEEP = 72,
+    H_W = 48, H_BETA = 52, H_SIGMA = 56, H_FLAGS = 60, H_SEED = 64, H_SWEEP = 72,
     H_STATS = 80 /* 4 x i64 */, H_CELLS = 112, H_ATOMS = 120, H_SUM = 128
 };
 
@@ -203,6 +203,7 @@ int pmc_snapshot_write(const char* path, const pmc_params* p, uint32_t next_swee
     put<float>(h, H_W, p->w);
     put<float>(h, H_BETA, p->beta);
     put<float>(h, H_SIGMA, p->sigma);
+    put<uint32_t>(h, H_FLAGS, p->flags);
     put<uint64_t>(h, H_SEED, p->seed);
     put<uint32_t>(h, H_SWEEP, next_sweep);
     const int64_t s4[4] = {st ? st->de_fixed : 0, st ? st->accepted : 0, st ? st->trials : 0, st ? st->evaluated : 0};
@@ -242,8 +243,13 @@ int pmc_snapshot_read(const char* path, pmc_params* p, uint32_t* next_sweep, pmc
     q.w = get<float>(h, H_W);
     q.beta = get<float>(h, H_BETA);
     q.sigma = get<float>(h, H_SIGMA);
+    q.flags = get<uint32_t>(h, H_FLAGS);
     q.seed = get<uint64_t>(h, H_SEED);
     const int64_t fcells = get<int64_t>(h, H_CELLS), atoms = get<int64_t>(h, H_ATOMS);
+    // the caller's buffers hold `cells` rows of 3*p->nmax floats: refuse any other nmax before
+    // writing anything (p is input here, the snapshot's parameters on return)
+    if ((h_disk || h_n) && (!p || p->nmax != q.nmax))
+        return pmc_io_fail(PMC_ERR_ARG, "pmc_snapshot_read: snapshot nmax differs from the buffer's (params->nmax)");
     if (p) *p = q;
     if (next_sweep) *next_sweep = get<uint32_t>(h, H_SWEEP);
     if (st) {

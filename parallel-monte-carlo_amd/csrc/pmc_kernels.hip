@@ -1126,51 +1126,258 @@ __global__ void k_assign_fill(DevGeom g, const float* __restrict__ r, int64_t n_
 
 // ------------------------------------------------------------------------------------------
 // total energy (calc_energy, kernel.cu:452-470) as a cell-list sum, fixed-point per pair
+//
+// One wave per owned cell.  The cell's stencil particles are staged into LDS (SoA, periodic image
+// added, compacted by ballot + mbcnt) in three groups: the own cell, the "mutual" forward
+// neighbours (owned, not wrapped, lexicographically after the cell: weight 2), and the directed
+// ones (wrapped across the periodic box or in a halo plane: weight 1).  A pair of mutual cells
+// gives bit-identical terms in both directions (xi - xj = -(xj - xi) exactly when no image is
+// added), so it is evaluated once and counted twice; a pair across a wrap or a slab boundary is
+// evaluated from each side like the oracle does (orc_energy: every directed pair, then x 0.5).  The
+// per-pair fixed-point terms (pmc_to_fixed_f32 = pmc_to_fixed((double)e), integer-only) are
+// summed in int64 -- exact in any order -- so the total equals the oracle's bit for bit.
+// Lanes run over the flattened (own particle i, staged partner j) pairs.
 // ------------------------------------------------------------------------------------------
+// Per-lane stencil description of one cell (lane k < 27: stencil cell k) for k_energy.
+struct EnergyStencil {
+    int kc;            // storage cell
+    float sx, sy, sz;  // periodic image
+    int grp;           // 0 own, 1 mutual forward (weight 2), 2 directed (weight 1), 3 skipped
+    int cnt;           // particles (0 for skipped cells); a load in flight until first used
+};
+
+__device__ __forceinline__ EnergyStencil energy_stencil(const DevGeom& g, const int16_t* __restrict__ ncnt,
+                                                        uint32_t t) {
+    const int lane = threadIdx.x & (kWave - 1);
+    // t is wave-uniform: scalar magic division (host-computed divisors)
+    const uint32_t q1 = udiv_magic(t, g.div_cx);          // t / cps_x
+    const uint32_t zq = udiv_magic(t, g.div_plane);       // t / (cps_x * cps_y)
+    const int x = (int)(t - q1 * (uint32_t)g.cps_x);
+    const int zl = (int)zq;
+    const int y = (int)(q1 - zq * (uint32_t)g.cps_y);
+    const int k = lane < 27 ? lane : 0;
+    const int hx = k / 9, hy = (k / 3) % 3, hz = k % 3;
+    const int dx = hx == 0 ? 0 : (hx == 1 ? -1 : 1);
+    const int dy = hy == 0 ? 0 : (hy == 1 ? -1 : 1);
+    const int dz = hz == 0 ? 0 : (hz == 1 ? -1 : 1);
+    EnergyStencil e;
+    int nx = x + dx, ny = y + dy;
+    e.sx = e.sy = e.sz = 0.0f;
+    if (nx < 0) { nx += g.cps_x; e.sx = -g.Lx; } else if (nx >= g.cps_x) { nx -= g.cps_x; e.sx = g.Lx; }
+    if (ny < 0) { ny += g.cps_y; e.sy = -g.Ly; } else if (ny >= g.cps_y) { ny -= g.cps_y; e.sy = g.Ly; }
+    const int zg = g.z0 + zl + dz;
+    if (zg < 0) e.sz = -g.Lz; else if (zg >= g.cps_z) e.sz = g.Lz;
+    const int nzl = g.halo ? zl + dz : (zl + dz + g.cps_z) % g.cps_z;
+    e.kc = (int)sidx(g, nx, ny, nzl);
+    const bool wrapped = e.sx != 0.0f || e.sy != 0.0f || e.sz != 0.0f;
+    const bool halo_nb = nzl < 0 || nzl >= g.nz_local;
+    const bool mutual = !wrapped && !halo_nb;
+    const bool forward = dz > 0 || (dz == 0 && (dy > 0 || (dy == 0 && dx > 0)));
+    e.grp = lane >= 27 ? 3 : (k == 0 ? 0 : (mutual ? (forward ? 1 : 3) : 2));
+    e.cnt = e.grp < 3 ? (int)ncnt[e.kc] : 0;
+    return e;
+}
+
+// fixed-point term of a listed pair: r2s = +r2 (weight 1) or -r2 (weight 2), r2 <= rc2 already
+// tested; the value is pmc_to_fixed((double)pmc_lj_from_r2(r2, rc2)) bit for bit
+__device__ __forceinline__ int64_t energy_term(float r2s, float r2min) {
+    const float r2 = __builtin_fabsf(r2s);
+    const float rr = r2 < r2min ? r2min : r2;
+    const float inv = pmc_recip(rr);
+    const float p6 = inv * inv * inv;
+    const int64_t e = pmc_to_fixed_f32(4.0f * (p6 * p6 - p6));
+    return __builtin_signbit(r2s) ? 2 * e : e;
+}
+
+// One wave per kEnergyCells consecutive owned cells.  Per cell: the stencil particles are staged
+// into LDS in three groups -- the own cell (all its slots first), the "mutual" forward neighbours
+// (owned, not wrapped, lexicographically after the cell: weight 2) and the directed ones (wrapped
+// across the periodic box or in a halo plane: weight 1); mutual backward neighbours are skipped.
+// A pair of mutual cells gives bit-identical terms in both directions (xi - xj = -(xj - xi)
+// exactly when no image is added), so it is evaluated once and counted twice; a pair across a
+// wrap or a slab boundary is evaluated from each side, as the oracle does (orc_energy: every
+// directed pair, then x 0.5).  Lanes run over the flattened pairs (own particle i, staged j > i);
+// the pairs inside the cutoff (about one in five) are listed in an LDS ring and only those are
+// converted: pmc_to_fixed_f32 per pair (= pmc_to_fixed((double)e)), int64 sums -- exact in any
+// order, so the total equals the oracle's bit for bit.  The next cell's rows are loaded while
+// the current cell's pairs run (the kernel is otherwise latency-bound: two dependent HBM round
+// trips per cell).
+constexpr int kEnergyCells = 8;
+
 template <int NSLOT>
-__global__ __launch_bounds__(256) void k_energy(DevGeom g, const float* __restrict__ disk,
-                                                const int16_t* __restrict__ ncnt,
-                                                unsigned long long* __restrict__ acc) {
-    constexpr int CPB = 256 / NSLOT;
-    const int p = threadIdx.x & (NSLOT - 1);
-    const int64_t t = (int64_t)blockIdx.x * CPB + threadIdx.x / NSLOT;
-    const int64_t total = (int64_t)g.cps_x * g.cps_y * g.nz_local;
+__global__ __launch_bounds__(kWave) void k_energy(DevGeom g, const float* __restrict__ disk,
+                                                  const int16_t* __restrict__ ncnt,
+                                                  unsigned long long* __restrict__ acc, uint32_t total_cells) {
+    extern __shared__ __attribute__((aligned(16))) float esm[];
+    constexpr int HS = NSLOT >= 16 ? 8 : NSLOT;       // staging lanes per cell (slots [0, HS))
+    constexpr int CPP = kWave / HS;                   // cells per staging pass
+    constexpr int NPMAX = (27 + CPP - 1) / CPP;
+    const int lane = threadIdx.x;
+    const int nm = g.nmax;
+    const int cap = 27 * nm;
+    float* ex_ = esm;
+    float* ey_ = esm + cap;
+    float* ez_ = esm + 2 * cap;
+    float* ring = esm + 3 * cap;                      // 128-entry ring of listed pairs (signed r2)
+    int* inv_l = (int*)(ring + 128);                  // list entry -> stencil lane (32 ints)
+    const int p = lane % HS;
+    const int ee = lane / HS;
+    const float rc2 = g.rc2;
+    const float r2min = g.r2min;
     long long sum = 0;
-    if (t < total) {
-        const int nm = g.nmax;
-        const int x = (int)(t % g.cps_x), y = (int)((t / g.cps_x) % g.cps_y);
-        const int zl = (int)(t / ((int64_t)g.cps_x * g.cps_y));
-        const int64_t c = sidx(g, x, y, zl);
-        if (p < ncnt[c]) {
-            const float xi = disk[c * 3 * nm + p], yi = disk[c * 3 * nm + nm + p], zi = disk[c * 3 * nm + 2 * nm + p];
-            for (int k = 0; k < 27; ++k) {
-                const int hx = k / 9, hy = (k / 3) % 3, hz = k % 3;
-                const int dx = hx == 0 ? 0 : (hx == 1 ? -1 : 1);
-                const int dy = hy == 0 ? 0 : (hy == 1 ? -1 : 1);
-                const int dz = hz == 0 ? 0 : (hz == 1 ? -1 : 1);
-                int nx = x + dx, ny = y + dy;
-                float sx = 0.0f, sy = 0.0f, sz = 0.0f;
-                if (nx < 0) { nx += g.cps_x; sx = -g.Lx; } else if (nx >= g.cps_x) { nx -= g.cps_x; sx = g.Lx; }
-                if (ny < 0) { ny += g.cps_y; sy = -g.Ly; } else if (ny >= g.cps_y) { ny -= g.cps_y; sy = g.Ly; }
-                const int zg = g.z0 + zl + dz;
-                if (zg < 0) sz = -g.Lz; else if (zg >= g.cps_z) sz = g.Lz;
-                const int nzl = g.halo ? zl + dz : (zl + dz + g.cps_z) % g.cps_z;
-                const int64_t cb = sidx(g, nx, ny, nzl);
-                const int cnt = ncnt[cb];
-                for (int q = 0; q < cnt; ++q) {
-                    if (k == 0 && q == p) continue;
-                    const float xj = disk[cb * 3 * nm + q] + sx;
-                    const float yj = disk[cb * 3 * nm + nm + q] + sy;
-                    const float zj = disk[cb * 3 * nm + 2 * nm + q] + sz;
-                    sum += pmc_to_fixed((double)pmc_lj_from_r2(pmc_r2(xi - xj, yi - yj, zi - zj), g.rc2));
+
+    const uint32_t t0 = blockIdx.x * (uint32_t)kEnergyCells;
+    const int ncl = (int)(total_cells - t0 < (uint32_t)kEnergyCells ? total_cells - t0 : (uint32_t)kEnergyCells);
+    // staged-cell list of the cell whose rows are in flight: entry -> stencil lane in inv_l,
+    // its group masks; rows in registers
+    float vx[NPMAX], vy[NPMAX], vz[NPMAX];
+    bool vact[NPMAX];
+    unsigned long long m0 = 0, m1 = 0, m2 = 0;
+    int n0 = 0, n1 = 0, ncells = 0;
+    auto issue_rows = [&](const EnergyStencil& st) {
+        m0 = __builtin_amdgcn_ballot_w64(st.grp == 0 && st.cnt > 0);
+        m1 = __builtin_amdgcn_ballot_w64(st.grp == 1 && st.cnt > 0);
+        m2 = __builtin_amdgcn_ballot_w64(st.grp == 2 && st.cnt > 0);
+        n0 = __popcll(m0);
+        n1 = __popcll(m1);
+        ncells = n0 + n1 + __popcll(m2);
+        const int pos = st.grp == 0 ? mbcnt64(m0) : (st.grp == 1 ? n0 + mbcnt64(m1) : n0 + n1 + mbcnt64(m2));
+        if (st.grp < 3 && st.cnt > 0) inv_l[pos] = lane;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        const int npass = (ncells + CPP - 1) / CPP;
+        const bool edge = __builtin_amdgcn_ballot_w64(st.sx != 0.0f || st.sy != 0.0f || st.sz != 0.0f) != 0;
+#pragma unroll
+        for (int q = 0; q < NPMAX; ++q) {
+            vact[q] = false;
+            if (q < npass) {
+                const int e = q * CPP + ee;
+                const int src = inv_l[e < ncells ? e : 0];
+                const int c_cnt = __shfl(st.cnt, src);
+                const int c_idx = __shfl(st.kc, src);
+                vact[q] = e < ncells && p < c_cnt;
+                const float* row = disk + (int64_t)c_idx * 3 * nm;
+                if (vact[q]) {
+                    vx[q] = row[p];
+                    vy[q] = row[nm + p];
+                    vz[q] = row[2 * nm + p];
+                }
+                if (edge) {   // periodic images (a +0 add changes no difference: interior cells skip it)
+                    // (cross-lane reads outside the branch: an inactive source lane supplies nothing)
+                    const float isx = __shfl(st.sx, src), isy = __shfl(st.sy, src), isz = __shfl(st.sz, src);
+                    vx[q] = vx[q] + isx;
+                    vy[q] = vy[q] + isy;
+                    vz[q] = vz[q] + isz;
                 }
             }
         }
+    };
+
+    EnergyStencil cur = energy_stencil(g, ncnt, t0);
+    issue_rows(cur);
+    EnergyStencil nxt = cur;
+    if (ncl > 1) nxt = energy_stencil(g, ncnt, t0 + 1);
+    for (int c = 0; c < ncl; ++c) {
+        // ---- stage cell c from the rows in registers: own cell (all slots), weight-2 cells,
+        //      then weight-1 cells (each group: main slots, then the fuller cells' slots [HS, n))
+        int S = 0;
+        auto put = [&](bool act, float ux, float uy, float uz) {
+            const unsigned long long am = __builtin_amdgcn_ballot_w64(act);
+            if (act) {
+                const int dst = S + mbcnt64(am);
+                ex_[dst] = ux;
+                ey_[dst] = uy;
+                ez_[dst] = uz;
+            }
+            S += __popcll(am);
+        };
+        auto overflow = [&](unsigned long long mg) {
+            if constexpr (HS < NSLOT) {
+                unsigned long long ov = __builtin_amdgcn_ballot_w64(((mg >> (lane & 63)) & 1ull) && cur.cnt > HS);
+                while (ov) {
+                    int ks = 0, nc = 0;
+                    for (; nc < CPP && ov; ++nc) {
+                        const int kb = (int)__builtin_ctzll(ov);
+                        ov &= ov - 1ull;
+                        ks = ee == nc ? kb : ks;
+                    }
+                    const int c_cnt = __shfl(cur.cnt, ks);
+                    const int c_idx = __shfl(cur.kc, ks);
+                    const float isx = __shfl(cur.sx, ks), isy = __shfl(cur.sy, ks), isz = __shfl(cur.sz, ks);
+                    const int ps = HS + p;
+                    const bool act = ee < nc && ps < c_cnt;
+                    float ux = 0.0f, uy = 0.0f, uz = 0.0f;
+                    if (act) {
+                        const float* row = disk + (int64_t)c_idx * 3 * nm;
+                        ux = row[ps] + isx;
+                        uy = row[nm + ps] + isy;
+                        uz = row[2 * nm + ps] + isz;
+                    }
+                    put(act, ux, uy, uz);
+                }
+            }
+        };
+        const int n_own = __builtin_amdgcn_readfirstlane(cur.cnt);   // lane 0 = own cell (entry 0)
+        const int e0 = n0 + n1;
+        // staged ranges: [0, n_own) own | main slots of the other cells in list order (weight-2
+        // cells first: [n_own, A)) | overflow slots of weight-2 cells [B, C) | of weight-1 cells
+        put(vact[0] && ee == 0, vx[0], vy[0], vz[0]);                 // own main slots
+        overflow(m0);                                                 // own slots [HS, n)
+        int A = S;
+#pragma unroll
+        for (int q = 0; q < NPMAX; ++q) {
+            const int e = q * CPP + ee;
+            if (q * CPP < ncells) {
+                A += __popcll(__builtin_amdgcn_ballot_w64(vact[q] && e >= 1 && e < e0));
+                put(vact[q] && e >= 1, vx[q], vy[q], vz[q]);
+            }
+        }
+        const int B = S;
+        overflow(m1);
+        const int C2 = S;
+        overflow(m2);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        // ---- the next cell's rows go out now and arrive while this cell's pairs run
+        if (c + 1 < ncl) {
+            cur = nxt;
+            issue_rows(cur);
+            if (c + 2 < ncl) nxt = energy_stencil(g, ncnt, t0 + (uint32_t)c + 2u);
+        }
+        if (n_own == 0) continue;
+        // ---- pairs (i, j): own particle i < n_own, staged j != i, flattened q = i*S + j (own-own
+        //      pairs in both directions, weight 1 each: bit-identical terms, like the oracle)
+        int head = 0, C = 0;   // ring: entries [head, head + C) mod 128
+        auto drain = [&](int lim) {
+            if (lane < lim) sum += energy_term(ring[(head + lane) & 127], r2min);
+            head = (head + 64) & 127;
+            C -= lim;
+        };
+        const int total = n_own * S;
+        const float inv_s = 1.0f / (float)S;
+        for (int q0 = 0; q0 < total; q0 += kWave) {
+            const int q = q0 + lane;
+            int i = (int)((float)q * inv_s);                // q / S, corrected below (q < 2^13)
+            int j = q - i * S;
+            i = j < 0 ? i - 1 : (j >= S ? i + 1 : i);
+            j = q - i * S;
+            const bool valid = q < total && j != i;
+            const int ii = valid ? i : 0;
+            const int jj = valid ? j : 0;
+            const float xi = ex_[ii], yi = ey_[ii], zi = ez_[ii];
+            const float xj = ex_[jj], yj = ey_[jj], zj = ez_[jj];
+            const float r2 = pmc_r2(xi - xj, yi - yj, zi - zj);
+            const bool in = valid && r2 <= rc2;
+            const bool w2 = (jj >= n_own && jj < A) || (jj >= B && jj < C2);
+            const unsigned long long im = __builtin_amdgcn_ballot_w64(in);
+            if (in) ring[(head + C + mbcnt64(im)) & 127] = w2 ? -r2 : r2;
+            C += __popcll(im);
+            if (C >= 64) drain(64);
+        }
+        if (C > 0) drain(C);
     }
     // wave sum (int64, exact in any order), one atomic per wave
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
-    if ((threadIdx.x & 63) == 0) atomicAdd(&acc[blockIdx.x & (kStatSlots - 1)], (unsigned long long)sum);
+    if (lane == 0) atomicAdd(&acc[blockIdx.x & (kStatSlots - 1)], (unsigned long long)sum);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1394,14 +1601,15 @@ hipError_t launch_assign(const DevGeom& g, const float* r, int64_t n_atoms, floa
 
 hipError_t launch_energy(const DevGeom& g, const float* disk, const int16_t* n,
                          unsigned long long* acc, hipStream_t st) {
-    const int64_t total = (int64_t)g.cps_x * g.cps_y * g.nz_local;
-    const int cpb = 256 / g.nslot;
-    dim3 grid((unsigned)((total + cpb - 1) / cpb)), block(256);
+    const int64_t total = (int64_t)g.cps_x * g.cps_y * g.nz_local;   // owned cells
+    const size_t lds = sizeof(float) * (3 * 27 * (size_t)g.nmax + 128 + 32);
+    dim3 grid((unsigned)((total + kEnergyCells - 1) / kEnergyCells)), block(kWave);
+    const uint32_t tc = (uint32_t)total;
     switch (g.nslot) {
-        case 8: hipLaunchKernelGGL(k_energy<8>, grid, block, 0, st, g, disk, n, acc); break;
-        case 16: hipLaunchKernelGGL(k_energy<16>, grid, block, 0, st, g, disk, n, acc); break;
-        case 32: hipLaunchKernelGGL(k_energy<32>, grid, block, 0, st, g, disk, n, acc); break;
-        default: hipLaunchKernelGGL(k_energy<64>, grid, block, 0, st, g, disk, n, acc); break;
+        case 8: hipLaunchKernelGGL(k_energy<8>, grid, block, lds, st, g, disk, n, acc, tc); break;
+        case 16: hipLaunchKernelGGL(k_energy<16>, grid, block, lds, st, g, disk, n, acc, tc); break;
+        case 32: hipLaunchKernelGGL(k_energy<32>, grid, block, lds, st, g, disk, n, acc, tc); break;
+        default: hipLaunchKernelGGL(k_energy<64>, grid, block, lds, st, g, disk, n, acc, tc); break;
     }
     return hipGetLastError();
 }

@@ -89,8 +89,9 @@ int main(int argc, char** argv) {
             total.evaluated += b.evaluated - a.evaluated;
             total.de_fixed += b.de_fixed - a.de_fixed;
         } else {
-            if ((rc = pmc_start(ctx, (uint32_t)s, k, &r))) die("pmc_start", rc);
-            e = r.e_final;
+            /* energies once per interval (for the trace line), not around every pmc_start */
+            if ((rc = pmc_start_ex(ctx, (uint32_t)s, k, PMC_START_NO_ENERGY, &r))) die("pmc_start_ex", rc);
+            if ((rc = pmc_energy(ctx, &e))) die("pmc_energy", rc);
             seconds += r.seconds;
             total.accepted += r.stats.accepted;
             total.trials += r.stats.trials;

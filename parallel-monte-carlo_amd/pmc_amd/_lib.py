@@ -24,7 +24,7 @@ class Params(C.Structure):
         ("nz_local", C.c_int32), ("z0", C.c_int32), ("halo", C.c_int32),
         ("nmax", C.c_int32), ("n_moves", C.c_int32),
         ("w", C.c_float), ("beta", C.c_float), ("sigma", C.c_float),
-        ("reserved", C.c_uint32), ("seed", C.c_uint64),
+        ("flags", C.c_uint32), ("seed", C.c_uint64),
     ]
 
 
@@ -45,6 +45,7 @@ class Result(C.Structure):
                 ("seconds", C.c_double), ("sweeps", C.c_int64)]
 
 
+PMC_FLAG_FULL_SHUFFLE = 1
 PMC_OK, PMC_ERR_ARG, PMC_ERR_HIP, PMC_ERR_OVERFLOW, PMC_ERR_RANGE, PMC_ERR_NODEV = 0, -1, -2, -3, -4, -5
 
 
@@ -124,9 +125,12 @@ def lib():
         _sig(L, "pmc_shift", i32, _vp, u32)
         _sig(L, "pmc_shift_slab", i32, _vp, u32, _vp)
         _sig(L, "pmc_start", i32, _vp, u32, i32, C.POINTER(Result))
+        _sig(L, "pmc_start_ex", i32, _vp, u32, i32, i32, C.POINTER(Result))
         _sig(L, "pmc_run_graph", i32, _vp, u32, i32)
         _sig(L, "pmc_sweep_plan", i32, C.c_uint64, u32, C.c_float, C.POINTER(C.c_int * 8), C.POINTER(C.c_int),
              C.POINTER(C.c_float))
+        _sig(L, "pmc_sweep_plan_ex", i32, C.c_uint64, u32, C.c_float, u32, C.POINTER(C.c_int * 8),
+             C.POINTER(C.c_int), C.POINTER(C.c_float))
         _sig(L, "pmc_energy", i32, _vp, C.POINTER(C.c_double))
         _sig(L, "pmc_stats_read", i32, _vp, C.POINTER(Stats), i32)
         _sig(L, "pmc_error_flags", i32, _vp, C.POINTER(C.c_uint32), i32)

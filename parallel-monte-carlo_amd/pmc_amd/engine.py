@@ -48,8 +48,8 @@ class PmcContext:
 
     def __init__(self, cps: int = 4, *, cps_y: int = 0, cps_z: int = 0, nz_local: int = 0, z0: int = 0,
                  halo: int = 0, nmax: int = 16, n_moves: int = 10, w: float = 2.5, beta: float = 0.3,
-                 sigma: float = 0.5, seed: int = 1234, stream: Optional[int] = None):
-        self.params = Params(cps, cps_y, cps_z, nz_local, z0, halo, nmax, n_moves, w, beta, sigma, 0, seed)
+                 sigma: float = 0.5, seed: int = 1234, stream: Optional[int] = None, flags: int = 0):
+        self.params = Params(cps, cps_y, cps_z, nz_local, z0, halo, nmax, n_moves, w, beta, sigma, flags, seed)
         h = C.c_void_p()
         check("pmc_create", lib().pmc_create(C.byref(self.params), C.byref(h)))
         self._h = h
@@ -62,6 +62,7 @@ class PmcContext:
         self.nmax = nmax
         self.n_moves = n_moves
         self.w = w
+        self.flags = flags
         self.cells = int(lib().pmc_storage_cells(self._h))
         if stream is not None:
             self.set_stream(stream)

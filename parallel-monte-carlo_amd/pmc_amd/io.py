@@ -70,6 +70,8 @@ def read_snapshot(path: str, cells: int | None = None):
         raise ValueError("cells: the number of cells stored (owned cells of the writer)")
     disk = np.empty(cells * 3 * p.nmax, np.float32)
     n = np.empty(cells, np.int16)
-    check("pmc_snapshot_read", lib().pmc_snapshot_read(str(path).encode(), None, None, None, disk.ctypes.data,
+    q = Params()
+    q.nmax = p.nmax          # the buffers' nmax (the reader refuses any other)
+    check("pmc_snapshot_read", lib().pmc_snapshot_read(str(path).encode(), C.byref(q), None, None, disk.ctypes.data,
                                                        n.ctypes.data, cells))
     return p, sw.value, st.as_dict(), disk, n

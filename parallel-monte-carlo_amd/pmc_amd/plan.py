@@ -10,9 +10,11 @@ import ctypes as C
 from ._lib import check, lib
 
 
-def sweep_plan(seed: int, sweep: int, w: float = 2.5):
+def sweep_plan(seed: int, sweep: int, w: float = 2.5, flags: int = 0):
+    """flags: pmc_params.flags (0: colours grouped by z parity; PMC_FLAG_FULL_SHUFFLE: all 8 shuffled)."""
     order = (C.c_int * 8)()
     f = C.c_int()
     d = C.c_float()
-    check("pmc_sweep_plan", lib().pmc_sweep_plan(seed, sweep, w, C.byref(order), C.byref(f), C.byref(d)))
+    check("pmc_sweep_plan_ex", lib().pmc_sweep_plan_ex(seed, sweep, w, flags, C.byref(order), C.byref(f),
+                                                       C.byref(d)))
     return list(order), f.value, d.value

@@ -167,3 +167,49 @@ def test_local_group_missing_rank_fails_not_hangs(pmc):
         d.ctx.slab_exchange()
     d.ctx.close()
     group.close()
+
+
+def test_c_slab_driver_one_chain_world4(pmc, oracle):
+    """PMC_SLAB_CHAINS=1 (one plane chain per rank: every phase one launch on the context stream),
+    world 4 through the in-process transport, equals the oracle's whole box.  Subprocess: the
+    switch is read once per process."""
+    import subprocess
+    import sys
+    code = r'''
+import sys, threading, numpy as np
+sys.path[:0] = [sys.argv[1], sys.argv[2], sys.argv[3]]
+import pmc_amd, pmc_oracle
+from test_gpu_multirank import _run_ranks, _window
+from pmc_amd.engine import LocalGroup
+from pmc_amd.slab import SlabDriver
+world, cps, nz, atoms = 4, 16, 4, 10000
+first = _window(pmc_oracle, 8)
+pmc_amd.lib()
+g = LocalGroup(world)
+keep = []
+def main(r):
+    d = SlabDriver(cps=cps, nz_local=nz, rank=r, world=world, atoms_total=atoms, local_group=g)
+    keep.append(d)
+    d.run(first, 8)
+    return d.owned(), d.ctx.stats()
+res = _run_ranks(world, main)
+st = pmc_oracle.OracleState(pmc_oracle.make_params(cps=cps))
+st.init_lattice(atoms)
+st.run(first, 8)
+plane, row = cps * cps, 48
+tot = {}
+for r, ((d, n), s) in enumerate(res):
+    ref = slice(r * nz * plane, (r + 1) * nz * plane)
+    assert np.array_equal(n, st.n[ref])
+    assert pmc_oracle.valid_slots_equal(d, n, st.disk[ref.start * row:ref.stop * row], st.n[ref], 16)
+    for k, v in s.items():
+        tot[k] = tot.get(k, 0) + v
+assert tot == st.stats.as_dict()
+print("ok")
+'''
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", code, os.path.join(repo, "parallel-monte-carlo_amd"),
+                          os.path.join(repo, "oracle"), os.path.join(repo, "tests")],
+                         env=dict(os.environ, PMC_SLAB_CHAINS="1"), capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "ok" in out.stdout

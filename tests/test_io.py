@@ -132,3 +132,26 @@ def test_snapshot_integrity(io, oracle, pmc, tmp_path):
     notsnap.write_bytes(b"hello world" * 20)
     with pytest.raises(pmc.PmcError, match="PMCSNAP1"):
         io.read_snapshot(notsnap, cells=0)
+
+
+def test_snapshot_read_refuses_other_nmax(io, oracle, pmc, tmp_path):
+    """The reader sizes nothing by the file: buffers for nmax 8 and a snapshot with nmax 10 are
+    refused before any write (pmc_io.cpp wrote past a smaller caller buffer)."""
+    import ctypes as C
+    import numpy as np
+    st = oracle.OracleState(oracle.make_params(cps=4, nmax=10))
+    st.init_lattice(64)
+    path = tmp_path / "s.pmcsnap"
+    io.write_snapshot(path, st.p, 7, {}, st.disk, st.n)
+    from pmc_amd._lib import Params, lib
+    q = Params()
+    q.nmax = 8
+    disk = np.full(st.cells * 3 * 8, 7.0, np.float32)
+    n = np.full(st.cells, 3, np.int16)
+    rc = lib().pmc_snapshot_read(str(path).encode(), C.byref(q), None, None, disk.ctypes.data, n.ctypes.data,
+                                 st.cells)
+    assert rc == -1                                       # PMC_ERR_ARG
+    assert "nmax" in lib().pmc_last_error().decode()
+    assert np.all(disk == 7.0) and np.all(n == 3)        # untouched
+    rc = lib().pmc_snapshot_read(str(path).encode(), None, None, None, disk.ctypes.data, n.ctypes.data, st.cells)
+    assert rc == -1                                       # buffers without params: refused

@@ -1,0 +1,14 @@
+#!/bin/bash
+# GPU box: the whole GPU test suite, the default bench line, the strong-scaling rehearsal at 8 and 4
+# ranks, and the energy timing.  Usage: bash tools/r02_check.sh <tag>
+set -o pipefail
+O=gpurun_out/$1; mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 150 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+timeout -k 10 300 python bench.py > $O/bench.log 2>&1 || { tail -30 $O/bench.log; exit 1; }
+grep '^{' $O/bench.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('bench value %.4g ms/step %.4f phase %s frac %s parity %s' % (d['value'], d['ms_per_step'], r['launch_ms'], r['frac'], (d.get('parity') or {}).get('state_bitwise_equal')))"
+for R in 8 4; do
+  timeout -k 10 200 python tools/strong_emulation.py --ranks $R > $O/strong$R.log 2>&1 || { tail -30 $O/strong$R.log; exit 1; }
+  grep '^{' $O/strong$R.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('strong R=%d full %.4f rank %.4f speedup %.2f host %.3f' % (d['ranks_emulated'], d['full_box_sweep_ms'], d['rank_sweep_ms'], d['projected_speedup'], d['host_issue_ms_per_sweep']))"
+done
+timeout -k 10 120 python tools/energy_timing.py
