@@ -35,6 +35,7 @@ struct pmc_ctx {
     uint32_t* flags = nullptr;
     int* ovf = nullptr;                    // subsweep overflow queue (1 + cells per colour)
     int* ovf_aux = nullptr;                // second queue: launches on a caller stream (pmc_phase_range_on)
+    int* ovf_b = nullptr;                  // third queue: the slab driver's boundary chain
     size_t ovf_bytes = 0;
     int32_t* tmp_cnt = nullptr;
     int32_t* tmp_idx = nullptr;
@@ -151,6 +152,7 @@ void drop_graph(pmc_ctx* c) {
 }
 
 void drop_slab(pmc_ctx* c);
+int slab_join(pmc_ctx* c);   // slab driver streams -> context stream (defined with the driver)
 
 // the next timing slot when pmc_timing is on (nullptr otherwise): events ride on the launch's
 // dispatch packet (hipExtLaunchKernelGGL), no extra packets in the stream
@@ -266,6 +268,7 @@ void pmc_destroy(pmc_ctx* c) {
     if (c->flags) (void)hipFree(c->flags);
     if (c->ovf) (void)hipFree(c->ovf);
     if (c->ovf_aux) (void)hipFree(c->ovf_aux);
+    if (c->ovf_b) (void)hipFree(c->ovf_b);
     if (c->tmp_cnt) (void)hipFree(c->tmp_cnt);
     if (c->tmp_idx) (void)hipFree(c->tmp_idx);
     if (c->d_r) (void)hipFree(c->d_r);
@@ -527,6 +530,7 @@ int pmc_run_graph(pmc_ctx* c, uint32_t first, int count) {
 
 int pmc_energy(pmc_ctx* c, double* e_out) {
     if (!c || !e_out) return fail(PMC_ERR_ARG, "bad argument");
+    if (int rj = slab_join(c)) return rj;
     PMC_HIP(hipMemsetAsync(c->eacc, 0, sizeof(unsigned long long) * kStatSlots, c->stream));
     hipError_t e = launch_energy(c->G, c->disk[c->cur], c->n[c->cur], c->eacc, c->stream);
     if (e != hipSuccess) return hip_fail(e, "energy launch");
@@ -542,6 +546,7 @@ int pmc_energy(pmc_ctx* c, double* e_out) {
 
 int pmc_stats_read(pmc_ctx* c, pmc_stats* out, int reset) {
     if (!c || !out) return fail(PMC_ERR_ARG, "bad argument");
+    if (int rj = slab_join(c)) return rj;
     std::vector<unsigned long long> h((size_t)kStatCounters * kStatSlots);
     PMC_HIP(hipMemcpyAsync(h.data(), c->stats, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost,
                            c->stream));
@@ -562,6 +567,7 @@ int pmc_stats_read(pmc_ctx* c, pmc_stats* out, int reset) {
 
 int pmc_error_flags(pmc_ctx* c, uint32_t* flags, int reset) {
     if (!c || !flags) return fail(PMC_ERR_ARG, "bad argument");
+    if (int rj = slab_join(c)) return rj;
     PMC_HIP(hipMemcpyAsync(flags, c->flags, 4, hipMemcpyDeviceToHost, c->stream));
     if (reset) PMC_HIP(hipMemsetAsync(c->flags, 0, 16, c->stream));
     PMC_HIP(hipStreamSynchronize(c->stream));
@@ -612,6 +618,7 @@ int pmc_start(pmc_ctx* c, uint32_t first, int mc_passes, pmc_result* out) {
 
 int pmc_copy_out(pmc_ctx* c, float* h_disk, int16_t* h_n) {
     if (!c) return fail(PMC_ERR_ARG, "null ctx");
+    if (int rj = slab_join(c)) return rj;
     if (h_disk) PMC_HIP(hipMemcpyAsync(h_disk, c->disk[c->cur], disk_bytes(c), hipMemcpyDeviceToHost, c->stream));
     if (h_n) PMC_HIP(hipMemcpyAsync(h_n, c->n[c->cur], n_bytes(c), hipMemcpyDeviceToHost, c->stream));
     PMC_HIP(hipStreamSynchronize(c->stream));
@@ -620,6 +627,7 @@ int pmc_copy_out(pmc_ctx* c, float* h_disk, int16_t* h_n) {
 
 int pmc_copy_in(pmc_ctx* c, const float* h_disk, const int16_t* h_n) {
     if (!c) return fail(PMC_ERR_ARG, "null ctx");
+    if (int rj = slab_join(c)) return rj;
     if (h_disk) PMC_HIP(hipMemcpyAsync(c->disk[c->cur], h_disk, disk_bytes(c), hipMemcpyHostToDevice, c->stream));
     if (h_n) PMC_HIP(hipMemcpyAsync(c->n[c->cur], h_n, n_bytes(c), hipMemcpyHostToDevice, c->stream));
     PMC_HIP(hipStreamSynchronize(c->stream));
@@ -628,6 +636,7 @@ int pmc_copy_in(pmc_ctx* c, const float* h_disk, const int16_t* h_n) {
 
 int pmc_synchronize(pmc_ctx* c) {
     if (!c) return fail(PMC_ERR_ARG, "null ctx");
+    if (int rj = slab_join(c)) return rj;
     PMC_HIP(hipStreamSynchronize(c->stream));
     return PMC_OK;
 }
@@ -690,6 +699,7 @@ int pmc_get_params(const pmc_ctx* c, pmc_params* out) {
 
 int pmc_stats_write(pmc_ctx* c, const pmc_stats* in) {
     if (!c || !in) return fail(PMC_ERR_ARG, "bad argument");
+    if (int rj = slab_join(c)) return rj;
     std::vector<unsigned long long> h((size_t)kStatCounters * kStatSlots, 0ull);
     h[0 * kStatSlots] = (unsigned long long)in->de_fixed;
     h[1 * kStatSlots] = (unsigned long long)in->accepted;
@@ -895,7 +905,7 @@ struct pmc_slab {
     int chains = 1;                       // plane chains (streams running subsweeps): 1 or 2
     hipEvent_t ev_i = nullptr, ev_b = nullptr, ev_t = nullptr;
     hipEvent_t ev_x = nullptr;            // T after its latest exchange
-    hipEvent_t ev_run[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};   // [chain][parity] run ends
+    hipEvent_t ev_run[3][2] = {{nullptr, nullptr}, {nullptr, nullptr}, {nullptr, nullptr}};   // [L, U, B][parity]
     std::vector<XferMsg> sends, recvs;    // the exchange being assembled
     bool messages() const { return comm != nullptr || group != nullptr; }
 };
@@ -914,11 +924,25 @@ void drop_slab(pmc_ctx* c) {
     if (s->aux) (void)hipStreamDestroy(s->aux);
     if (s->hi) (void)hipStreamSynchronize(s->hi);
     for (hipEvent_t e : {s->ev_i, s->ev_b, s->ev_t, s->ev_x, s->ev_run[0][0], s->ev_run[0][1], s->ev_run[1][0],
-                         s->ev_run[1][1]})
+                         s->ev_run[1][1], s->ev_run[2][0], s->ev_run[2][1]})
         if (e) (void)hipEventDestroy(e);
     if (s->hi) (void)hipStreamDestroy(s->hi);
     delete s;
     c->slab = nullptr;
+}
+
+// order the context stream after all work of the slab driver's other streams (before the state, the
+// halos or the statistics are read on it)
+int slab_join(pmc_ctx* c) {
+    pmc_slab* s = c->slab;
+    if (!s) return PMC_OK;
+    for (hipStream_t st : {s->aux, s->hi}) {
+        if (!st) continue;
+        hipError_t e = hipEventRecord(s->ev_b, st);
+        if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, s->ev_b, 0);
+        if (e != hipSuccess) return hip_fail(e, "slab join");
+    }
+    return PMC_OK;
 }
 
 // queue one message of the current exchange
@@ -1110,41 +1134,51 @@ int slab_attach(pmc_ctx* c, int rank, int world, bool messages) {
     s->below = (rank + world - 1) % world;
     s->above = (rank + 1) % world;
     hipError_t e;
-    if ((e = hipStreamCreateWithFlags(&s->aux, hipStreamNonBlocking)) != hipSuccess) {
+    // the boundary chain (T) is the critical path of a sweep when its small launches wait for the
+    // interior chains' waves to retire: its queue gets the higher dispatch priority
+    // (PMC_SLAB_PRIORITY=0 disables)
+    static const bool prio = [] {
+        const char* v = std::getenv("PMC_SLAB_PRIORITY");
+        return !(v && std::atoi(v) == 0);
+    }();
+    int lo_p = 0, hi_p = 0;
+    if (prio) (void)hipDeviceGetStreamPriorityRange(&lo_p, &hi_p);
+    if ((e = hipStreamCreateWithPriority(&s->aux, hipStreamNonBlocking, prio ? hi_p : 0)) != hipSuccess) {
         drop_slab(c);
         return hip_fail(e, "hipStreamCreate");
     }
     for (hipEvent_t* ev : {&s->ev_i, &s->ev_b, &s->ev_t, &s->ev_x, &s->ev_run[0][0], &s->ev_run[0][1],
-                           &s->ev_run[1][0], &s->ev_run[1][1]})
+                           &s->ev_run[1][0], &s->ev_run[1][1], &s->ev_run[2][0], &s->ev_run[2][1]})
         if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) {
             drop_slab(c);
             return hip_fail(e, "hipEventCreate");
         }
-    // Two plane chains (lower and upper half of the slab on two streams) when the halves keep the
-    // checkerboard parity (nz % 4 == 0); PMC_SLAB_CHAINS=1 forces one.
+    // Interior planes in two chains (lower and upper part on two streams); PMC_SLAB_CHAINS=1: one
+    // chain (the upper part empty, every interior launch on the context stream)
     {
         static const int forced = [] {
             const char* v = std::getenv("PMC_SLAB_CHAINS");
             return v ? std::atoi(v) : 0;
         }();
-        s->chains = (c->P.nz_local % 4 == 0 && forced != 1) ? 2 : 1;
+        s->chains = forced == 1 ? 1 : 2;
     }
-    if (s->chains == 2 && (e = hipStreamCreateWithFlags(&s->hi, hipStreamNonBlocking)) != hipSuccess) {
+    if ((e = hipStreamCreateWithFlags(&s->hi, hipStreamNonBlocking)) != hipSuccess) {
         drop_slab(c);
         return hip_fail(e, "hipStreamCreate");
     }
     // every "latest" event starts recorded (waits on them are no-ops until real work records them)
-    for (hipEvent_t ev : {s->ev_x, s->ev_run[0][0], s->ev_run[0][1], s->ev_run[1][0], s->ev_run[1][1]})
+    for (hipEvent_t ev : {s->ev_x, s->ev_run[0][0], s->ev_run[0][1], s->ev_run[1][0], s->ev_run[1][1],
+                          s->ev_run[2][0], s->ev_run[2][1]})
         if ((e = hipEventRecord(ev, c->stream)) != hipSuccess) {
             drop_slab(c);
             return hip_fail(e, "hipEventRecord");
         }
-    if (!c->ovf_aux) {   // the boundary launches' overflow queue (they run beside the interior's)
-        if ((e = hipMalloc(&c->ovf_aux, c->ovf_bytes)) != hipSuccess || (e = hipMemset(c->ovf_aux, 0, c->ovf_bytes)) != hipSuccess) {
+    // overflow queues of the upper and the boundary chain (they run beside the context stream's)
+    for (int** q : {&c->ovf_aux, &c->ovf_b})
+        if (!*q && ((e = hipMalloc(q, c->ovf_bytes)) != hipSuccess || (e = hipMemset(*q, 0, c->ovf_bytes)) != hipSuccess)) {
             drop_slab(c);
             return hip_fail(e, "hipMalloc overflow queue");
         }
-    }
     (void)messages;   // halo messages go straight from and into the state buffers
     return PMC_OK;
 }
@@ -1217,118 +1251,143 @@ int pmc_slab_init_local(pmc_ctx* c, int rank, pmc_local_group* g) {
 int pmc_slab_exchange(pmc_ctx* c) {
     if (!c || !c->slab) return fail(PMC_ERR_ARG, "no slab driver (pmc_slab_init)");
     pmc_slab* s = c->slab;
+    // everything before (state set up on the context stream, earlier sweeps on all three streams)
+    // is ordered before the exchange and before every stream's next work
+    int rc = slab_join(c);
+    if (rc) return rc;
     PMC_HIP(hipEventRecord(s->ev_i, c->stream));
     PMC_HIP(hipStreamWaitEvent(s->aux, s->ev_i, 0));
-    int rc = slab_exchange_full(c);
-    if (rc) return rc;
+    PMC_HIP(hipStreamWaitEvent(s->hi, s->ev_i, 0));
+    if ((rc = slab_exchange_full(c))) return rc;
     PMC_HIP(hipEventRecord(s->ev_t, s->aux));
-    PMC_HIP(hipEventRecord(s->ev_x, s->aux));
     PMC_HIP(hipStreamWaitEvent(c->stream, s->ev_t, 0));
+    PMC_HIP(hipStreamWaitEvent(s->hi, s->ev_t, 0));
+    for (hipEvent_t ev : {s->ev_x, s->ev_run[0][0], s->ev_run[0][1], s->ev_run[1][0], s->ev_run[1][1],
+                          s->ev_run[2][0], s->ev_run[2][1]})
+        PMC_HIP(hipEventRecord(ev, s->aux));
     return PMC_OK;
 }
 
 int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
     if (!c || !c->slab) return fail(PMC_ERR_ARG, "no slab driver (pmc_slab_init)");
     pmc_slab* s = c->slab;
-    hipStream_t S = c->stream, T = s->aux;
+    hipStream_t S = c->stream, U = s->hi, T = s->aux;
     const int nz = c->P.nz_local;
-    const int m = s->chains;
-    hipStream_t chain[2] = {S, s->hi};
-    int* queue[2] = {c->ovf, c->ovf_aux};
-    const int zlo[2] = {0, m == 2 ? nz / 2 : nz}, zhi[2] = {m == 2 ? nz / 2 : nz, nz};
+    // interior planes [1, nz-1): lower chain L = [1, zs) on S, upper chain U = [zs, nz-1) on its own
+    // stream; zs is even so every parity-q run of L ends at the same side of the split
+    int zs = 2 * (nz / 4);
+    if (s->chains == 1 || zs < 2) zs = nz - 1;                 // one interior chain (or none: nz = 2)
     const pmc_sweep_plan_t plan = pmc_plan_for_sweep_ex(c->P.seed, sweep, c->P.w, c->P.flags);
-    hipError_t e;
     int rc;
     // The 8 colour phases form runs of equal z parity q (two runs of 4 with the default plan).  In a
     // run only the planes of parity q change, each reading its own plane and the parity 1-q planes
     // next to it, which no phase of the run writes and no halo of the run changes: every plane's
-    // chain of phases is independent of the other planes' for the whole run.  So the slab's planes
-    // are split into m = 2 chains (lower half [0, nz/2) on the context stream, upper half on a
-    // second stream) that run each run's phases without any synchronisation between them -- one
-    // chain's launch gaps and tails overlap the other's work -- and synchronise only where a run's
-    // reads cross the split or a halo:
-    //   * a parity-1 run on the lower chain reads plane nz/2 (upper chain), a parity-0 run on the
-    //     upper chain reads plane nz/2-1 (lower chain): they wait for the other chain's previous run;
-    //   * at the end of a run of parity q the boundary plane P_q (plane 0 for q = 0, nz-1 for q = 1,
-    //     written by the lower resp. upper chain) goes whole to the neighbour rank holding it as a halo
-    //     and the matching halo H_q comes from the other side, on the exchange stream T
-    //     (slab_exchange_run), after the producing chain's run and the reading chain's previous run;
-    //   * the chain that reads H_q (the upper one for q = 0: top halo; the lower one for q = 1) waits
-    //     for that exchange before its next run.
-    // Cells of a colour are independent, so any split of a phase gives the whole-box result bit for
-    // bit (the GPU tests compare every world size with the oracle's whole box).
-    PMC_HIP(hipEventRecord(s->ev_i, S));                         // S after the previous sweep's shift
-    if (m == 2) PMC_HIP(hipStreamWaitEvent(chain[1], s->ev_i, 0));
+    // chain of phases is independent of the other planes' for the whole run.  So each run is three
+    // independent chains of launches:
+    //   L (context stream S): the run's phases on interior planes [1, zs);
+    //   U (second stream):    the run's phases on interior planes [zs, nz-1);
+    //   B (exchange stream T): the run's phases on the boundary plane P_q (plane 0 for q = 0, nz-1
+    //     for q = 1) -- the only plane of the run that reads a halo (H_{1-q}, received by T at the end
+    //     of the previous run) and that another rank holds as a halo -- then the exchange: P_q whole to
+    //     the neighbour holding it, H_q from the other side (slab_exchange_run), one message each way.
+    // L's and U's launch gaps and tails overlap each other's work, and the exchange overlaps both.
+    // The chains synchronise only at run boundaries, where a run's reads cross a chain border (with
+    // zs even: q = 1: L's plane 1 reads plane 0 (B's), L's plane zs-1 reads plane zs (U's), B's plane
+    // nz-1 reads plane nz-2 (U's); q = 0: U's plane zs reads plane zs-1 (L's), U's plane nz-2 reads
+    // plane nz-1 (B's), B's plane 0 reads plane 1 (L's)): each waits for the owner chain's previous
+    // run (an event per chain and parity; border_waits derives the set from the plane ownership, so
+    // one interior chain or none works the same way).  Those are also the only readers of the
+    // planes a run overwrites, so the same waits order every overwrite after its readers.  Cells of a colour are independent, so any split of a phase gives the whole-box
+    // result bit for bit (the GPU tests compare every world size with the oracle's whole box).
+    enum { kL = 0, kU = 1, kB = 2 };
     int k = 0;
-    bool first_run = true;
-    while (k < 8) {
-        const int q = plan.order[k] % 2;                         // itoa: offset[2] = colour % 2
-        int k1 = k;
-        while (k1 < 8 && plan.order[k1] % 2 == q) ++k1;          // run [k, k1)
-        for (int j = 0; j < m; ++j) {
-            hipStream_t st = chain[j];
-            if (m == 2 && !first_run) {
-                if (q == 1 && j == 0) PMC_HIP(hipStreamWaitEvent(st, s->ev_run[1][0], 0));
-                if (q == 0 && j == 1) PMC_HIP(hipStreamWaitEvent(st, s->ev_run[0][1], 0));
-            }
-            // the halo this run reads (H_{1-q}: bottom for q = 0, top for q = 1) is received by T
-            const int halo_reader = q == 0 ? 0 : m - 1;
-            if (j == halo_reader) PMC_HIP(hipStreamWaitEvent(st, s->ev_x, 0));
-            for (int kk = k; kk < k1; ++kk) {
-                int o[3];
-                pmc_colour_offset(plan.order[kk], o);
-                LaunchTiming lt;
-                e = launch_subsweep(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep, c->stats, queue[j],
-                                    zlo[j], zhi[j], st, next_timing(c, j == 0 ? 0 : 2, &lt));
-                if (e != hipSuccess) return hip_fail(e, "subsweep launch");
-            }
-            PMC_HIP(hipEventRecord(s->ev_run[j][q], st));
+    auto phases = [&](hipStream_t st, int* ovf, int z0, int z1, int k0, int k1, int kind) -> int {
+        for (int kk = k0; kk < k1; ++kk) {
+            int o[3];
+            pmc_colour_offset(plan.order[kk], o);
+            LaunchTiming lt;
+            hipError_t le = kind == kB
+                ? launch_subsweep_boundary(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep, c->stats,
+                                           ovf, z0, z1, nullptr, 0, st, next_timing(c, 2, &lt))
+                : launch_subsweep(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep, c->stats, ovf, z0,
+                                  z1, st, next_timing(c, kind == kL ? 0 : 2, &lt));
+            if (le != hipSuccess) return hip_fail(le, "subsweep launch");
         }
-        // exchange of P_q / H_q: after the producing chain's run and the H_q reader's previous run
-        const int producer = q == 0 ? 0 : m - 1;
-        const int hq_reader = q == 0 ? m - 1 : 0;
-        PMC_HIP(hipStreamWaitEvent(T, s->ev_run[producer][q], 0));
-        PMC_HIP(hipStreamWaitEvent(T, s->ev_run[hq_reader][1 - q], 0));
+        return PMC_OK;
+    };
+    // owner chain of owned plane z; the planes a chain writes in a run of parity q and the other
+    // chains owning a plane next to one of them (those it waits for; halos are T's own business)
+    auto owner = [&](int z) { return (z == 0 || z == nz - 1) ? (int)kB : (z < zs ? (int)kL : (int)kU); };
+    auto border_waits = [&](int chain, int z0, int z1, int q, hipStream_t st, int parity) -> int {
+        bool need[3] = {false, false, false};
+        for (int z = z0; z < z1; ++z) {
+            if ((z & 1) != q) continue;
+            for (int zn : {z - 1, z + 1})
+                if (zn >= 0 && zn < nz && owner(zn) != chain) need[owner(zn)] = true;
+        }
+        for (int j = 0; j < 3; ++j)
+            if (need[j]) PMC_HIP(hipStreamWaitEvent(st, s->ev_run[j][parity], 0));
+        return PMC_OK;
+    };
+    while (k < 8) {
+        const int q = plan.order[k] % 2;                          // itoa: offset[2] = colour % 2
+        int k1 = k;
+        while (k1 < 8 && plan.order[k1] % 2 == q) ++k1;           // run [k, k1)
+        const int p = 1 - q;                                      // parity of the previous run
+        // L
+        if ((rc = border_waits(kL, 1, zs, q, S, p))) return rc;
+        if (zs > 1 && (rc = phases(S, c->ovf, 1, zs, k, k1, kL))) return rc;
+        PMC_HIP(hipEventRecord(s->ev_run[kL][q], S));
+        // U
+        if ((rc = border_waits(kU, zs, nz - 1, q, U, p))) return rc;
+        if (nz - 1 > zs && (rc = phases(U, c->ovf_aux, zs, nz - 1, k, k1, kU))) return rc;
+        PMC_HIP(hipEventRecord(s->ev_run[kU][q], U));
+        // B, then the exchange
+        const int zb = q == 0 ? 0 : nz - 1;
+        if ((rc = border_waits(kB, zb, zb + 1, q, T, p))) return rc;
+        if ((rc = phases(T, c->ovf_b, zb, zb + 1, k, k1, kB))) return rc;
+        PMC_HIP(hipEventRecord(s->ev_run[kB][q], T));
         if ((rc = slab_exchange_run(c, q))) return rc;
-        PMC_HIP(hipEventRecord(s->ev_x, T));
-        first_run = false;
         k = k1;
     }
-    // shiftCells reads every plane and both halos: join both chains and T
-    if (m == 2) {
-        PMC_HIP(hipEventRecord(s->ev_b, chain[1]));
-        PMC_HIP(hipStreamWaitEvent(S, s->ev_b, 0));
-    }
+    // shiftCells reads every plane and both halos: join U and T into S.  (Splitting the shift over
+    // the three chains measured slower: the boundary chain, whose small launches wait for the
+    // interior chains' waves, is the last to finish a sweep, and its share of the shift came after.)
+    PMC_HIP(hipEventRecord(s->ev_b, U));
+    PMC_HIP(hipStreamWaitEvent(S, s->ev_b, 0));
+    PMC_HIP(hipEventRecord(s->ev_x, T));
     PMC_HIP(hipStreamWaitEvent(S, s->ev_x, 0));
-    // shiftCells: after the 8 phases both halo planes are exact copies of the
-    // neighbours' planes, so every halo plane whose new content depends only on planes this rank
-    // holds is shifted here, bit-identical to its owner's result.  Along x or y that is both halo
-    // planes (no exchange at all); along z in direction dir, the halo on the -dir side (it takes
-    // particles from the owned plane next to it), and the other one is received: one plane with
-    // its counts, one direction, instead of both planes.
+    // after the 8 phases both halo planes are exact copies of the neighbours' planes, so
+    // every halo plane whose new content depends only on planes this rank holds is shifted here,
+    // bit-identical to its owner's result.  Along x or y that is both halo planes (no exchange at
+    // all); along z in direction dir, the halo on the -dir side (it takes particles from the owned
+    // plane next to it), and the other one is received: one plane with its counts, one direction.
     int zl0, zl1;
     const int dir = slab_shift_planes(nz, plan, &zl0, &zl1);
     LaunchTiming lts;
-    e = launch_shift_planes(c->G, c->disk[c->cur], c->n[c->cur], c->disk[c->cur ^ 1], c->n[c->cur ^ 1], plan.f,
-                            plan.d, c->flags, zl0, zl1, S, next_timing(c, 1, &lts));
+    hipError_t e = launch_shift_planes(c->G, c->disk[c->cur], c->n[c->cur], c->disk[c->cur ^ 1], c->n[c->cur ^ 1],
+                                       plan.f, plan.d, c->flags, zl0, zl1, S, next_timing(c, 1, &lts));
     if (e != hipSuccess) return hip_fail(e, "shift launch");
     c->cur ^= 1;
-    // the next sweep's first boundary launch follows the shift on T ("I(-1)" wait); its first
-    // interior reads no halo, so it overlaps the z exchange
-    // T after the shift: the exchanges of the next sweep and the z halo read/write the new buffer
+    // U and T continue after the shift (it rewrote every plane); the z halo arrives on T, overlapping
+    // the next sweep's first interior launches (they read no halo)
+    // (the chains' "previous run" events all point at the shift: the next sweep's border waits then
+    // cost nothing -- in particular none waits for the z halo, which only B reads, in T order)
     PMC_HIP(hipEventRecord(s->ev_i, S));
+    PMC_HIP(hipStreamWaitEvent(U, s->ev_i, 0));
     PMC_HIP(hipStreamWaitEvent(T, s->ev_i, 0));
+    for (int j = 0; j < 3; ++j) {
+        PMC_HIP(hipEventRecord(s->ev_run[j][0], S));
+        PMC_HIP(hipEventRecord(s->ev_run[j][1], S));
+    }
     if (dir != 0 && (rc = slab_exchange_zplane(c, dir))) return rc;
     PMC_HIP(hipEventRecord(s->ev_x, T));
-    PMC_HIP(hipEventRecord(s->ev_t, T));
     return PMC_OK;
 }
 
 int pmc_slab_finish(pmc_ctx* c) {
     if (!c || !c->slab) return fail(PMC_ERR_ARG, "no slab driver (pmc_slab_init)");
-    PMC_HIP(hipEventRecord(c->slab->ev_t, c->slab->aux));
-    PMC_HIP(hipStreamWaitEvent(c->stream, c->slab->ev_t, 0));
-    return PMC_OK;
+    return slab_join(c);
 }
 
 int pmc_timing_kinds(pmc_ctx* c, int enable, double ms[3], int count[3]) {
@@ -1338,6 +1397,7 @@ int pmc_timing_kinds(pmc_ctx* c, int enable, double ms[3], int count[3]) {
     if (!c->tkind.empty()) {
         PMC_HIP(hipStreamSynchronize(c->stream));
         if (c->slab) PMC_HIP(hipStreamSynchronize(c->slab->aux));
+        if (c->slab && c->slab->hi) PMC_HIP(hipStreamSynchronize(c->slab->hi));
         for (size_t k = 0; k < c->tkind.size(); ++k) {
             float t = 0.0f;
             PMC_HIP(hipEventElapsedTime(&t, c->tev[2 * k], c->tev[2 * k + 1]));

@@ -909,8 +909,13 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_fallback(DevGeom
         (void)subsweep_wave<NSLOT, NMC, 27 * NMC, OFF32, MIRROR>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, full,
                                                                  full, t, cz0, mirror, mirror_mode);
     }
-    // the last workgroup to finish (every workgroup has read the count by then) clears the queue
-    // for the next launch: no memset between launches, and graph replays start from a clean queue
+    // the queue is cleared for the next launch (no memset between launches; graph replays start
+    // from a clean queue): a one-workgroup grid clears it itself; otherwise the last workgroup to
+    // finish (every workgroup has read the count by then) does
+    if (gridDim.x == 1) {
+        if (threadIdx.x == 0 && count != 0) ovf[kOvfCount] = 0;
+        return;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         __threadfence();
@@ -1435,9 +1440,19 @@ static void launch_k(K kernel, dim3 grid, dim3 block, size_t lds, hipStream_t st
     else hipLaunchKernelGGL(kernel, grid, block, lds, st, args...);
 }
 
-#ifndef PMC_FALLBACK_BLOCKS
-#define PMC_FALLBACK_BLOCKS 64   // fixed grid of the overflow launch (it strides over the queue)
-#endif
+// Grid of the overflow launch (it strides over the queue).  The queue is empty in almost every
+// phase (a cell overflows the main launch's LDS capacity only if its filtered stencil holds more
+// than kMainCap partners); the launch costs the same ~5 us of dispatch with 1, 8 or 64 workgroups
+// (kernel trace, tools/strong_trace.sh), so 8 (one per XCD) spread a crowded queue at no cost.
+// PMC_FALLBACK_BLOCKS=n overrides (n = 1: no completion atomics at all).
+static unsigned fallback_blocks() {
+    static const unsigned n = [] {
+        const char* v = std::getenv("PMC_FALLBACK_BLOCKS");
+        const int k = v ? std::atoi(v) : 8;
+        return (unsigned)(k > 0 ? k : 1);
+    }();
+    return n;
+}
 int subsweep_capacity(const DevGeom& g) {
     // Partners per wave held in LDS by the main launch.  Sized so a wave needs at most 5 KiB of
     // LDS (-> 32 waves/CU, the hardware limit): 3 floats per partner (x, y, z) + 2 term-list
@@ -1467,7 +1482,7 @@ static void launch_subsweep_t(const DevGeom& g, float* disk, const int16_t* n, i
              ox, oy, oz, sweep, stats, cap, ovf, cz0, ncz);
     if (cap < full) {
         const size_t lds_full = sizeof(float) * (size_t)lds_floats_per_wave(full) * kSubWaves;
-        hipLaunchKernelGGL((k_subsweep_fallback<NSLOT, NMC, OFF32>), dim3(PMC_FALLBACK_BLOCKS), dim3(kWave * kSubWaves), lds_full, st,
+        hipLaunchKernelGGL((k_subsweep_fallback<NSLOT, NMC, OFF32>), dim3(fallback_blocks()), dim3(kWave * kSubWaves), lds_full, st,
                            g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0);
     }
 }
@@ -1486,11 +1501,11 @@ static void launch_direct_t(const DevGeom& g, float* disk, const int16_t* n, int
     if (cap < full) {
         const size_t lds_full = sizeof(float) * (size_t)lds_floats_per_wave(full) * kSubWaves;
         if (mirror)
-            hipLaunchKernelGGL((k_subsweep_fallback<NSLOT, NMC, OFF32, true>), dim3(PMC_FALLBACK_BLOCKS),
+            hipLaunchKernelGGL((k_subsweep_fallback<NSLOT, NMC, OFF32, true>), dim3(fallback_blocks()),
                                dim3(kWave * kSubWaves), lds_full, st, g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0,
                                mirror, mode);
         else
-            hipLaunchKernelGGL((k_subsweep_fallback<NSLOT, NMC, OFF32>), dim3(PMC_FALLBACK_BLOCKS),
+            hipLaunchKernelGGL((k_subsweep_fallback<NSLOT, NMC, OFF32>), dim3(fallback_blocks()),
                                dim3(kWave * kSubWaves), lds_full, st, g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0,
                                nullptr, 0);
     }
