@@ -350,6 +350,14 @@ int orc_shift_cells(const pmc_params* p, const float* din, const int16_t* nin, f
  * compute from its own data, pmc_shift_slab). */
 int orc_shift_cells_planes(const pmc_params* p, const float* din, const int16_t* nin, float* dout,
                            int16_t* nout, int f, float d, int zl_begin, int zl_end) {
+    /* the planes must be stored, and along z in a slab each plane's dir-neighbour too (a halo
+     * plane on the +dir side cannot be computed locally: it is received) -- found by the
+     * sanitizer build (asan_main.c), which reads past the storage otherwise */
+    if (f < 0 || f > 2 || zl_begin < -p->halo || zl_end > p->nz_local + p->halo || zl_end < zl_begin) return -1;
+    if (f == 2 && p->halo) {
+        const int dir = (d <= 0) ? -1 : 1;
+        if (zl_begin + dir < -1 || zl_end - 1 + dir > p->nz_local) return -1;
+    }
     const int nm = p->nmax;
     const float w = p->w;
     const int cps[3] = {p->cps_x, p->cps_y, p->cps_z};

@@ -42,6 +42,8 @@ void orc_subsweep_range(const pmc_params* p, float* disk, const int16_t* n, int 
 /* shiftCells (CUDA-Parallel-MC/CUDA-Parallel-MC/shiftCells.h:23-112) -- returns overflow count */
 int orc_shift_cells(const pmc_params* p, const float* din, const int16_t* nin, float* dout,
                     int16_t* nout, int f, float d);
+/* over local planes [zl_begin, zl_end) (halo planes included); -1 for a range outside the storage
+ * or, along z in a slab, one whose dir-neighbour plane is not stored */
 int orc_shift_cells_planes(const pmc_params* p, const float* din, const int16_t* nin, float* dout,
                            int16_t* nout, int f, float d, int zl_begin, int zl_end);
 /* calc_energy (kernel.cu:452-470) as a cell-list sum over owned cells */

@@ -1576,6 +1576,10 @@ hipError_t launch_shift_planes(const DevGeom& g, const float* din, const int16_t
                                int16_t* nout, int f, float d, uint32_t* flags, int zl_begin, int zl_end,
                                hipStream_t st, const LaunchTiming* tm) {
     if (zl_begin < -g.halo || zl_end > g.nz_local + g.halo || zl_end <= zl_begin) return hipErrorInvalidValue;
+    if (f == 2 && g.halo) {   // along z each plane reads its dir-neighbour, which must be stored
+        const int dir = (d <= 0) ? -1 : 1;
+        if (zl_begin + dir < -1 || zl_end - 1 + dir > g.nz_local) return hipErrorInvalidValue;
+    }
 #ifndef PMC_SHIFT_U
 #define PMC_SHIFT_U 8
 #endif

@@ -172,14 +172,23 @@ def test_odd_colour_count_parity(pmc, oracle, cps):
         assert r[k] == o[k], k
 
 
-def test_graph_replay_equals_eager(pmc):
+def test_graph_replay_equals_oracle(pmc, oracle):
+    """pmc_run_graph (the sweep loop start.cu:237-260 captured as one hipGraph and replayed, SURVEY
+    8f row 4) equals the C oracle bit for bit -- every occupied slot, counts, the four counters --
+    over 6 sweeps replayed as 2 + 4 (two graphs), and equals eager launches byte for byte."""
     a = _ctx(pmc, 16)
     b = _ctx(pmc, 16)
     a.init_lattice(10_000)
     b.init_lattice(10_000)
-    for s in range(4):
+    for s in range(6):
         a.sweep(s)
-    b.run_graph(0, 4)
+    b.run_graph(0, 2)
+    b.run_graph(2, 4)
+    st = _ostate(oracle, 16)
+    st.init_lattice(10_000)
+    assert st.run(0, 6) == 0
+    _assert_same(oracle, b, st, 16)
+    assert b.stats() == st.stats.as_dict()
     da, na = a.copy_out()
     db, nb = b.copy_out()
     assert np.array_equal(na, nb) and np.array_equal(da.view(np.uint32), db.view(np.uint32))
