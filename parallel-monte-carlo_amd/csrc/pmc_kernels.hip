@@ -862,11 +862,12 @@ __global__ __launch_bounds__(kWave * kSubWaves) __attribute__((amdgpu_waves_per_
 #endif
 }
 
-// Boundary-plane launch of the slab driver: the main launch's two-cell waves and capacity (5 KiB of
-// LDS per wave: its waves wait for the interior's to retire and then stay resident as long as the
-// interior runs, so they must not hold more LDS than an interior wave), written-back rows mirrored
-// into the halo exchange buffer; cells over the capacity go to its own queue, which a mirroring
-// fallback launch on the same stream visits.
+// Boundary-plane launch of the slab driver: ONE cell per wave at the main launch's capacity (5 KiB
+// of LDS per wave).  The boundary chain's launches are single colour planes that run beside the
+// interior chains' launches and wait for their waves to retire; a boundary phase then takes about
+// one wave lifetime, which one cell per wave halves (the two-cell waves of the main launch only pay
+// off when a launch is many rounds of waves long).  Cells over the capacity go to the queue `ovf`,
+// which the fallback launch after it visits.  Written-back rows may also go to `mirror`.
 template <int NSLOT, int NMC, bool OFF32>
 __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_direct(DevGeom g, float* __restrict__ disk,
                                                                          const int16_t* __restrict__ ncnt,
@@ -879,14 +880,16 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_direct(DevGeom g
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     float* px_ = smem + wv * lds_floats_per_wave(kMainCap);
     const int total = (g.cps_x >> 1) * (g.cps_y >> 1) * ncz;
-    const int t = 2 * ((int)blockIdx.x * kSubWaves + wv);    // two cells per wave
+    const int t = (int)blockIdx.x * kSubWaves + wv;
     if (t >= total) return;
+    bool ok;
     if (mirror)
-        subsweep_pair<NSLOT, NMC, kMainCap, OFF32, true>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, kMainCap, cap, t,
-                                                         t + 1 < total, cz0, ovf, mirror, mirror_mode);
+        ok = subsweep_wave<NSLOT, NMC, kMainCap, OFF32, true>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, kMainCap,
+                                                             cap, t, cz0, mirror, mirror_mode);
     else
-        subsweep_pair<NSLOT, NMC, kMainCap, OFF32>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, kMainCap, cap, t,
-                                                   t + 1 < total, cz0, ovf);
+        ok = subsweep_wave<NSLOT, NMC, kMainCap, OFF32>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, kMainCap, cap,
+                                                       t, cz0);
+    if (!ok && (threadIdx.x & (kWave - 1)) == 0) ovf[kOvfHead + atomicAdd(&ovf[kOvfCount], 1)] = t;
 }
 
 // Fallback launch: full capacity (27*nmax partners per wave), a fixed grid striding over the
@@ -1480,7 +1483,11 @@ static void launch_subsweep_t(const DevGeom& g, float* disk, const int16_t* n, i
     const size_t lds = sizeof(float) * (size_t)lds_floats_per_wave(kMainCap) * kSubWaves;
     launch_k(k_subsweep<NSLOT, NMC, OFF32>, dim3((unsigned)blocks), dim3(kWave * kSubWaves), lds, st, tm, g, disk, n,
              ox, oy, oz, sweep, stats, cap, ovf, cz0, ncz);
+#ifdef PMC_PROBE_NO_FALLBACK   // timing probe only (wrong results if a cell overflows)
+    if (false) {
+#else
     if (cap < full) {
+#endif
         const size_t lds_full = sizeof(float) * (size_t)lds_floats_per_wave(full) * kSubWaves;
         hipLaunchKernelGGL((k_subsweep_fallback<NSLOT, NMC, OFF32>), dim3(fallback_blocks()), dim3(kWave * kSubWaves), lds_full, st,
                            g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0);
@@ -1492,13 +1499,17 @@ static void launch_direct_t(const DevGeom& g, float* disk, const int16_t* n, int
                             unsigned long long* stats, int* ovf, int cz0, int ncz, float* mirror, int mode,
                             hipStream_t st, const LaunchTiming* tm) {
     const int64_t total = (int64_t)(g.cps_x / 2) * (g.cps_y / 2) * ncz;
-    const int64_t blocks = ((total + 1) / 2 + kSubWaves - 1) / kSubWaves;   // two cells per wave
+    const int64_t blocks = (total + kSubWaves - 1) / kSubWaves;   // one cell per wave
     const int cap = subsweep_capacity(g);
     const int full = 27 * g.nmax;
     const size_t lds = sizeof(float) * (size_t)lds_floats_per_wave(kMainCap) * kSubWaves;
     launch_k(k_subsweep_direct<NSLOT, NMC, OFF32>, dim3((unsigned)blocks), dim3(kWave * kSubWaves), lds, st, tm, g,
              disk, n, ox, oy, oz, sweep, stats, cap, ovf, cz0, ncz, mirror, mode);
+#ifdef PMC_PROBE_NO_FALLBACK   // timing probe only (wrong results if a cell overflows)
+    if (false) {
+#else
     if (cap < full) {
+#endif
         const size_t lds_full = sizeof(float) * (size_t)lds_floats_per_wave(full) * kSubWaves;
         if (mirror)
             hipLaunchKernelGGL((k_subsweep_fallback<NSLOT, NMC, OFF32, true>), dim3(fallback_blocks()),
