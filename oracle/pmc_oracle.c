@@ -37,6 +37,7 @@ int orc_params_check(pmc_params* p) {
     if (p->flags & ~PMC_FLAG_FULL_SHUFFLE) return PMC_ERR_ARG;
     if (!p->halo && (p->nz_local != p->cps_z || p->z0 != 0)) return PMC_ERR_ARG;
     if (p->z0 < 0 || p->z0 + p->nz_local > p->cps_z) return PMC_ERR_ARG;
+    if (!(p->beta >= 0.0f) || isinf(p->beta)) return PMC_ERR_ARG;
     return PMC_OK;
 }
 

@@ -89,6 +89,7 @@ int normalise(pmc_params* p) {
         return fail(PMC_ERR_ARG, "halo == 0 requires the whole box (nz_local == cps_z, z0 == 0)");
     if (p->z0 < 0 || p->z0 + p->nz_local > p->cps_z) return fail(PMC_ERR_ARG, "slab outside the box");
     if (!(p->w > 0.0f) || !(p->sigma >= 0.0f)) return fail(PMC_ERR_ARG, "w must be > 0, sigma >= 0");
+    if (!(p->beta >= 0.0f) || std::isinf(p->beta)) return fail(PMC_ERR_ARG, "beta must be finite and >= 0");
     const int64_t cells = (int64_t)p->cps_x * p->cps_y * (p->nz_local + 2 * p->halo);
     if (cells * 3 * p->nmax >= ((int64_t)1 << 32)) return fail(PMC_ERR_ARG, "box too large (2^32 coordinate slots per context)");
     if ((int64_t)p->cps_x * p->cps_y * p->cps_z > 0xFFFFFFFFll) return fail(PMC_ERR_ARG, "more than 2^32 cells");
@@ -110,6 +111,7 @@ DevGeom make_geom(const pmc_params& p) {
     g.rc2 = pmc_cutoff_r2(p.w);
     g.rc2f = pmc_filter_r2(g.rc2);
     g.r2min = PMC_R2_MIN;
+    g.inv_b4 = p.beta > 0.0f ? 1.0 / (4.0 * (double)p.beta) : 0.0;   // the acceptance bound's estimate
     g.div_ncx = make_udiv_magic((uint32_t)(p.cps_x / 2));
     g.div_ncy = make_udiv_magic((uint32_t)(p.cps_y / 2));
     g.div_cx = make_udiv_magic((uint32_t)p.cps_x);

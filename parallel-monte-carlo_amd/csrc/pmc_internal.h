@@ -50,6 +50,7 @@ struct DevGeom {
     float w, beta, sigma, Lx, Ly, Lz, rc2;
     float rc2f;                    // staging filter threshold (pmc_filter_r2)
     float r2min;                   // PMC_R2_MIN (passed as data so the kernel keeps it in an SGPR)
+    double inv_b4;                 // 1 / (4*(double)beta), 0 for beta == 0 (accept_bound's estimate)
     UDivMagic div_ncx, div_ncy;    // division by cps_x/2 and cps_y/2 (subsweep cell decode)
     UDivMagic div_cx, div_plane;   // division by cps_x and cps_x*cps_y (energy cell decode)
     uint32_t rk0[10], rk1[10];     // Philox round keys k + r*W (kernel arguments -> SGPRs, no key adds)

@@ -164,6 +164,26 @@ __device__ __forceinline__ uint32_t udiv_magic(uint32_t n, UDivMagic m) {
     return (hi + ((n - hi) >> m.sh1)) >> m.sh2;
 }
 
+// Acceptance by one float compare.  accept_move (subsweep.h:209-216; the spec's form, kept by the
+// oracle) accepts when beta*dE < T in double, and the product of two floats is exact in double.
+// The moves reduce s = dE/4, so for beta > 0 that is b4 * s < T with b4 = 4*(double)beta (24
+// significant bits: b4 * s is exact too), i.e. s <= F with F the largest float whose product with
+// b4 is below T.  F from the estimate T * (1/b4) (within one float ulp of T/b4), then one ulp step
+// either way, checked exactly; the parking lanes do this once per move, off the moves' serial
+// path.  beta == 0 (normalise rejects beta < 0): 0 < T always, as F = +inf gives for the finite s
+// the r2 floor guarantees.
+__device__ __forceinline__ float accept_bound(float T, const DevGeom& g) {
+    if (!(g.beta > 0.0f)) return __builtin_inff();
+    const double Td = (double)T;
+    const double b4 = 4.0 * (double)g.beta;
+    const float f = (float)(Td * g.inv_b4);                        // >= 0 (T > 0), maybe +inf
+    const float up = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, f) + 1u);
+    const float dn = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, f) - 1u);
+    const bool f_ok = (double)f * b4 < Td;                          // false for +inf
+    const bool up_ok = (double)up * b4 < Td;                        // false for NaN (f = +inf)
+    return f_ok ? (up_ok ? up : f) : dn;
+}
+
 // storage index of local cell (x, y, zl)
 __device__ __forceinline__ int64_t sidx(const DevGeom& g, int x, int y, int zl) {
     return (int64_t)x + (int64_t)g.cps_x * ((int64_t)y + (int64_t)g.cps_y * (int64_t)(zl + g.halo));
@@ -329,7 +349,7 @@ __device__ __forceinline__ void rng_chunk_single(const DevGeom& g, uint32_t id, 
     pmc_det_sincos_2pi(pmc_u01(ws), &sn, &cs);
     const float G0 = (R * cs) * g.sigma;   // lanes 0-15: d0 of move m0+j; 32-47: d2
     const float G1 = (R * sn) * g.sigma;   // lanes 0-15: d1
-    const float TT = -lg;                  // lanes 16-31: T
+    const float TT = accept_bound(-lg, g);    // lanes 16-31: T's acceptance bound
     if (lane < 16) *(float2*)(py_ + lcap4 + 2 * j) = make_float2(G0, G1);
     else if (lane < 48) pz_[lcap4 + 2 * j + (lane < 32 ? 1 : 0)] = lane < 32 ? TT : G0;
 }
@@ -508,14 +528,13 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
     const float cxf = (float)x * g.w - g.Lx / 2.0f + hw;
     const float cyf = (float)y * g.w - g.Ly / 2.0f + hw;
     const float czf = (float)zg0 * g.w - g.Lz / 2.0f + hw;
-    const double beta_d = (double)g.beta;
     const float rc2 = g.rc2;
     const float nrc2 = -g.rc2;
     // PMC_R2_MIN through an SGPR: v_max_f32 |r2s|, s takes it with the free |.| modifier (a
     // literal operand would force a second max)
     const float r2min = as_f(wave_uniform(as_i(g.r2min)));
 
-    double de_cell = 0.0;
+    double de_cell = 0.0;   // sum of the accepted moves' s = dE/4 (x4 at the end: exact)
     int n_acc = 0, n_ev = 0;
     int i = 0;
     // ---- 4. trial moves --------------------------------------------------------------------
@@ -567,7 +586,7 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
                 const float* slot = mvs + 2 * (r0 + j);
                 const float2 qa = *(const float2*)slot;             // (qx, qy)
                 const float2 qb = *(const float2*)(slot + stride);  // (qz, T)
-                const float qx = qa.x, qy = qa.y, qz = qb.x, Tm = qb.y;
+                const float qx = qa.x, qy = qa.y, qz = qb.x, Fm = qb.y;   // Fm: T's acceptance bound
                 const int si = __builtin_amdgcn_readlane(sp_l, j);  // S_nb + particle of move j
                 const float xi = px_[si], yi = py_[si], zi = pz_[si];
                 ++n_ev;
@@ -577,22 +596,26 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
                 // ~80% of staged pairs lie beyond rc for a given position; they are exactly 0
                 // and never reach the reciprocal.
                 int C = 0;   // wave-uniform
+                // list one block's terms: the new-position ones within the cutoff, then the
+                // old-position ones (negated r2, sign bit set), compacted by ballot + mbcnt
+                auto list = [&](float r2n, float r2on) {
+                    const unsigned long long mn = __builtin_amdgcn_ballot_w64(r2n <= rc2);
+                    const unsigned long long mo = __builtin_amdgcn_ballot_w64(r2on >= nrc2);
+                    const int cn = C + __popcll(mn);
+                    // exec-masked stores (2 SALU each) beat a select into a discard slot (one
+                    // half-rate v_cndmask per list on gfx950); packed f32 for the distances
+                    // (lo/hi = two blocks) measured 5% slower (v_pk_*_f32 issue at half rate)
+                    if (__builtin_amdgcn_inverse_ballot_w64(mn)) buf[mbcnt64_add(mn, C)] = r2n;
+                    if (__builtin_amdgcn_inverse_ballot_w64(mo)) buf[mbcnt64_add(mo, cn)] = r2on;
+                    C = cn + __popcll(mo);
+                };
                 auto block = [&](int base) {
                     // slots >= K and the moving slot hold +inf in x: their r2 is inf, never listed
                     const int k = base + lane;
                     const float xj = px_[k], yj = py_[k], zj = pz_[k];
                     // old-position term computed negated (= -r2o bit for bit, pmc_r2_neg):
                     // listed with its sign bit set at no extra instruction
-                    const float r2n = pmc_r2(qx - xj, qy - yj, qz - zj);
-                    const float r2on = pmc_r2_neg(xi - xj, yi - yj, zi - zj);
-                    const unsigned long long mn = __builtin_amdgcn_ballot_w64(r2n <= rc2);
-                    const unsigned long long mo = __builtin_amdgcn_ballot_w64(r2on >= nrc2);
-                    const int cn = C + __popcll(mn);
-                    // exec-masked stores (2 SALU each) beat a select into a discard slot (one
-                    // half-rate v_cndmask per list on gfx950)
-                    if (__builtin_amdgcn_inverse_ballot_w64(mn)) buf[mbcnt64_add(mn, C)] = r2n;
-                    if (__builtin_amdgcn_inverse_ballot_w64(mo)) buf[mbcnt64_add(mo, cn)] = r2on;
-                    C = cn + __popcll(mo);
+                    list(pmc_r2(qx - xj, qy - yj, qz - zj), pmc_r2_neg(xi - xj, yi - yj, zi - zj));
                 };
                 if constexpr (NB > 0) {
 #pragma unroll
@@ -625,19 +648,21 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
                 }
 #endif
                 buf[C + lane] = kPad;
-                // the first pass unconditionally (C == 0 reads only kPad: +0), the rest looped
-                float acc = 0.0f + lj4_signed_max(buf[lane], r2min);
+                // the first pass unconditionally (C == 0 reads only kPad: +0), the rest looped.  (A
+                // lane sum may start at -0 where the oracle's starts 0 + -0 = +0: zeros of either
+                // sign leave every nonzero sum, the accept test and de_cell unchanged.)
+                float acc = lj4_signed_max(buf[lane], r2min);
                 for (int t0 = kWave; t0 < C; t0 += kWave) acc = acc + lj4_signed_max(buf[t0 + lane], r2min);
-                // quarter energies were accumulated; the factor 4 is exact, so 4*(sum of u)
-                // equals the sum of the 4u the oracle accumulates, bit for bit
-                const float dEu = wave_sum_fixed_order_s(4.0f * acc);   // SGPR
-                const bool acc_mv = beta_d * (double)dEu < (double)Tm;   // accept_move, subsweep.h:209-216
+                // quarter energies u are accumulated and reduced: s = dE/4.  Scaling by 4 is exact,
+                // so dE = 4s equals the oracle's sum of the 4u, bit for bit, in any association
+                const float sq = wave_sum_fixed_order_s(acc);           // SGPR
+                const bool acc_mv = sq <= Fm;                            // accept_move, subsweep.h:209-216
                 px_[si] = acc_mv ? qx : xi;                              // (every lane, same value)
                 if (acc_mv) {
                     py_[si] = qy;
                     pz_[si] = qz;
                     ++n_acc;
-                    de_cell = de_cell + (double)dEu;
+                    de_cell = de_cell + (double)sq;
                 }
             }
             i += L;
@@ -674,7 +699,7 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
         }
     }
     // fixed-point conversion only when something was accepted (pmc_to_fixed(0) == 0)
-    const int64_t de_fix = n_acc ? pmc_to_fixed(de_cell) : 0;
+    const int64_t de_fix = n_acc ? pmc_to_fixed(4.0 * de_cell) : 0;
 #ifdef PMC_PROBE_NO_STATS   // timing probe only (the counters stay zero): cost of the stats atomics
     if (lane == 0 && de_fix == 0x7fffffffffffffffll) {
 #else
@@ -793,7 +818,7 @@ __device__ __forceinline__ void subsweep_pair(const DevGeom& g, float* __restric
     pmc_det_sincos_2pi(pmc_u01(ws), &sn, &cs);
     const float G0 = (R * cs) * g.sigma;          // l < 10: d0; 10-19: d2
     const float G1 = (R * sn) * g.sigma;          // l < 10: d1
-    const float TT = -lg;                         // 20-29: T
+    const float TT = accept_bound(-lg, g);           // 20-29: T's acceptance bound
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     const int fyw = (int)*(const uint32_t*)(buf + (h >> 1) + (l & 15));
     const int jv = (int)pmc_bounded((uint32_t)fyw, (uint32_t)((l & 15) + 1));
@@ -1480,7 +1505,10 @@ static void launch_subsweep_t(const DevGeom& g, float* disk, const int16_t* n, i
     const int64_t blocks = (waves + kSubWaves - 1) / kSubWaves;
     const int cap = subsweep_capacity(g);
     const int full = 27 * g.nmax;
-    const size_t lds = sizeof(float) * (size_t)lds_floats_per_wave(kMainCap) * kSubWaves;
+    size_t lds = sizeof(float) * (size_t)lds_floats_per_wave(kMainCap) * kSubWaves;
+#ifdef PMC_PROBE_LDS_MULT   // timing probe only: fewer waves per SIMD through a larger LDS request
+    lds = lds * PMC_PROBE_LDS_MULT / 100;
+#endif
     launch_k(k_subsweep<NSLOT, NMC, OFF32>, dim3((unsigned)blocks), dim3(kWave * kSubWaves), lds, st, tm, g, disk, n,
              ox, oy, oz, sweep, stats, cap, ovf, cz0, ncz);
 #ifdef PMC_PROBE_NO_FALLBACK   // timing probe only (wrong results if a cell overflows)

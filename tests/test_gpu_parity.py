@@ -138,6 +138,27 @@ def test_full_sweeps_parity_16(pmc, oracle):
     assert abs(r["e_initial"] + r["de_fixed"] / 2**32 - r["e_final"]) < 1e-3 * abs(r["e_final"])
 
 
+@pytest.mark.parametrize("beta", [0.0, 1e-30, 0.3, 7.5, 3e37])
+def test_acceptance_paths_parity(pmc, oracle, beta):
+    """accept_move (subsweep.h:209-216) on the device is one float compare of s = dE/4 against a
+    per-move bound F (largest float with 4*beta*F < T, parked by the RNG lanes; +inf for beta = 0);
+    it equals the oracle's beta*dE < T in double bit for bit.  beta = 0: every evaluated move is
+    accepted (pyramid step 5 on the GPU); 1e-30: the bound estimates overflow to +inf and clamp to
+    FLT_MAX; 3e37: 4*beta overflows float (the bound works in double)."""
+    ctx = _ctx(pmc, 16, beta=beta)
+    ctx.init_lattice(10_000)
+    st = _ostate(oracle, 16, beta=beta)
+    st.init_lattice(10_000)
+    r = ctx.start(0, 3)
+    assert st.run(0, 3) == 0
+    _assert_same(oracle, ctx, st, 16)
+    o = st.stats.as_dict()
+    for k in ("de_fixed", "accepted", "trials", "evaluated"):
+        assert r[k] == o[k], k
+    if beta == 0.0:
+        assert r["accepted"] == r["evaluated"] > 0
+
+
 @pytest.mark.parametrize("n_moves", [0, 1, 7, 11, 23, 42])
 def test_move_count_chunking_parity(pmc, oracle, n_moves):
     """Move counts across the RNG chunk boundaries (the two-cell prologue parks 10 moves per cell,

@@ -336,3 +336,12 @@ def test_oracle_sanitizers_clean(oracle):
                                 UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1"))
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
     assert r.stdout.strip().endswith("clean")
+
+
+@pytest.mark.parametrize("beta", [-0.1, float("inf"), float("nan")])
+def test_params_reject_bad_beta(oracle, beta):
+    """beta must be finite and >= 0 (the library's normalise() refuses the same)."""
+    st_params = oracle.make_params(cps=4, beta=beta)
+    with pytest.raises(Exception):
+        oracle.OracleState(st_params)
+
