@@ -15,11 +15,14 @@ agg = collections.defaultdict(list)
 for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         if r["Kernel_Name"].split("(")[0].split("<")[0] == "k_subsweep":
-            agg[(r["Dispatch_Id"], r["Counter_Name"])].append(float(r["Counter_Value"]))
+            agg[((f, r["Dispatch_Id"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
 per = collections.defaultdict(list)
 for (d, c), v in agg.items():
     per[c].append(sum(v))
-for c in sorted(per):
-    v = per[c]
-    print(f"{c:28s} mean per dispatch {sum(v)/len(v):14.1f}   n={len(v)}")
+mean = {c: sum(v) / len(v) for c, v in per.items()}
+for c in sorted(mean):
+    print(f"{c:28s} mean per dispatch {mean[c]:14.1f}   n={len(per[c])}")
+cells = 2 * mean.get("SQ_WAVES", 0)   # two cells per wave in the main launch
+if cells:
+    print("per cell visit: " + ", ".join(f"{c} {mean[c] / cells:.1f}" for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS") if c in mean))
 PY
