@@ -229,6 +229,25 @@ def test_single_colour_parity_64(pmc, oracle):
     assert ctx.stats() == st.stats.as_dict()
 
 
+def test_full_sweeps_parity_128(pmc, oracle):
+    """BASELINE config 3 (128^3 cells, 1e7 particles): two full sweeps -- all 8 colour phases and
+    shiftCells, one shift along z -- compared with the oracle bit for bit (every occupied slot,
+    counts, the four counters, the energy).  Tolerance: none."""
+    oracle.set_threads(16)
+    s0 = next(s for s in range(100) if oracle.sweep_plan(1234, s, 2.5)[1] == 2)
+    ctx = _ctx(pmc, 128)
+    ctx.init_lattice(10_000_000)
+    st = _ostate(oracle, 128)
+    st.init_lattice(10_000_000)
+    r = ctx.start(s0, 2)
+    assert st.run(s0, 2) == 0
+    _assert_same(oracle, ctx, st, 16)
+    o = st.stats.as_dict()
+    for k in ("de_fixed", "accepted", "trials", "evaluated"):
+        assert r[k] == o[k], k
+    assert r["e_final"] == st.energy()
+
+
 def test_single_colour_parity_128(pmc, oracle):
     """BASELINE config 3 size: 128^3 cells, 1e7 particles; one colour phase compared bitwise,
     then size-independent properties over full sweeps."""
