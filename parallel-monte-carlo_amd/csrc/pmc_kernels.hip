@@ -1177,6 +1177,7 @@ struct EnergyStencil {
     float sx, sy, sz;  // periodic image
     int grp;           // 0 own, 1 mutual forward (weight 2), 2 directed (weight 1), 3 skipped
     int cnt;           // particles (0 for skipped cells); a load in flight until first used
+    int x, y, zg;      // the cell (wave-uniform): its box filters the staged partners
 };
 
 __device__ __forceinline__ EnergyStencil energy_stencil(const DevGeom& g, const int16_t* __restrict__ ncnt,
@@ -1189,19 +1190,23 @@ __device__ __forceinline__ EnergyStencil energy_stencil(const DevGeom& g, const 
     const int zl = (int)zq;
     const int y = (int)(q1 - zq * (uint32_t)g.cps_y);
     const int k = lane < 27 ? lane : 0;
-    const int hx = k / 9, hy = (k / 3) % 3, hz = k % 3;
-    const int dx = hx == 0 ? 0 : (hx == 1 ? -1 : 1);
-    const int dy = hy == 0 ? 0 : (hy == 1 ? -1 : 1);
-    const int dz = hz == 0 ? 0 : (hz == 1 ? -1 : 1);
+    // lane k = 9*hx + 3*hy + hz, h = 0, 1, 2 -> offset 0, -1, +1 (the subsweep's stencil masks)
+    const int dx = (int)bit_of(kStencilPos[0], k) - (int)bit_of(kStencilNeg[0], k);
+    const int dy = (int)bit_of(kStencilPos[1], k) - (int)bit_of(kStencilNeg[1], k);
+    const int dz = (int)bit_of(kStencilPos[2], k) - (int)bit_of(kStencilNeg[2], k);
     EnergyStencil e;
-    int nx = x + dx, ny = y + dy;
-    e.sx = e.sy = e.sz = 0.0f;
-    if (nx < 0) { nx += g.cps_x; e.sx = -g.Lx; } else if (nx >= g.cps_x) { nx -= g.cps_x; e.sx = g.Lx; }
-    if (ny < 0) { ny += g.cps_y; e.sy = -g.Ly; } else if (ny >= g.cps_y) { ny -= g.cps_y; e.sy = g.Ly; }
-    const int zg = g.z0 + zl + dz;
-    if (zg < 0) e.sz = -g.Lz; else if (zg >= g.cps_z) e.sz = g.Lz;
-    const int nzl = g.halo ? zl + dz : (zl + dz + g.cps_z) % g.cps_z;
-    e.kc = (int)sidx(g, nx, ny, nzl);
+    e.x = x;
+    e.y = y;
+    e.zg = g.z0 + zl;
+    // periodic wrap as selects, 32-bit storage index (< 2^31 storage cells, normalise)
+    const int nx0 = x + dx, ny0 = y + dy, zg = g.z0 + zl + dz, nz0 = zl + dz;
+    const int nx = nx0 + (nx0 < 0 ? g.cps_x : 0) - (nx0 >= g.cps_x ? g.cps_x : 0);
+    const int ny = ny0 + (ny0 < 0 ? g.cps_y : 0) - (ny0 >= g.cps_y ? g.cps_y : 0);
+    e.sx = nx0 < 0 ? -g.Lx : (nx0 >= g.cps_x ? g.Lx : 0.0f);
+    e.sy = ny0 < 0 ? -g.Ly : (ny0 >= g.cps_y ? g.Ly : 0.0f);
+    e.sz = zg < 0 ? -g.Lz : (zg >= g.cps_z ? g.Lz : 0.0f);
+    const int nzl = g.halo ? nz0 : nz0 + (nz0 < 0 ? g.cps_z : 0) - (nz0 >= g.cps_z ? g.cps_z : 0);
+    e.kc = nx + g.cps_x * (ny + g.cps_y * (nzl + g.halo));
     const bool wrapped = e.sx != 0.0f || e.sy != 0.0f || e.sz != 0.0f;
     const bool halo_nb = nzl < 0 || nzl >= g.nz_local;
     const bool mutual = !wrapped && !halo_nb;
@@ -1237,7 +1242,7 @@ __device__ __forceinline__ int64_t energy_term(float r2s, float r2min) {
 // trips per cell).
 constexpr int kEnergyCells = 8;
 
-template <int NSLOT>
+template <int NSLOT, bool OFF32>
 __global__ __launch_bounds__(kWave) void k_energy(DevGeom g, const float* __restrict__ disk,
                                                   const int16_t* __restrict__ ncnt,
                                                   unsigned long long* __restrict__ acc, uint32_t total_cells) {
@@ -1288,11 +1293,12 @@ __global__ __launch_bounds__(kWave) void k_energy(DevGeom g, const float* __rest
                 const int c_cnt = __shfl(st.cnt, src);
                 const int c_idx = __shfl(st.kc, src);
                 vact[q] = e < ncells && p < c_cnt;
-                const float* row = disk + (int64_t)c_idx * 3 * nm;
                 if (vact[q]) {
-                    vx[q] = row[p];
-                    vy[q] = row[nm + p];
-                    vz[q] = row[2 * nm + p];
+                    using DA = DiskAddr<OFF32>;
+                    const uint32_t off = ((uint32_t)c_idx * (uint32_t)(3 * nm) + (uint32_t)p) * DA::kUnit;
+                    vx[q] = DA::ld(disk, off);
+                    vy[q] = DA::ld(disk, off + (uint32_t)nm * DA::kUnit);
+                    vz[q] = DA::ld(disk, off + 2u * (uint32_t)nm * DA::kUnit);
                 }
                 if (edge) {   // periodic images (a +0 add changes no difference: interior cells skip it)
                     // (cross-lane reads outside the branch: an inactive source lane supplies nothing)
@@ -1312,6 +1318,12 @@ __global__ __launch_bounds__(kWave) void k_energy(DevGeom g, const float* __rest
     for (int c = 0; c < ncl; ++c) {
         // ---- stage cell c from the rows in registers: own cell (all slots), weight-2 cells,
         //      then weight-1 cells (each group: main slots, then the fuller cells' slots [HS, n))
+        // partners farther than the cutoff from every point of the own cell's (padded) box
+        // contribute exactly 0 to every pair with an own particle: not staged (the subsweep's
+        // conservative filter, pmc_box_d2); own particles always are
+        float blo[3], bhi[3];
+        pmc_cell_box(cur.x, cur.y, cur.zg, g.w, g.Lx, g.Ly, g.Lz, blo, bhi);
+        auto near = [&](float ux, float uy, float uz) { return pmc_box_d2(ux, uy, uz, blo, bhi) <= g.rc2f; };
         int S = 0;
         auto put = [&](bool act, float ux, float uy, float uz) {
             const unsigned long long am = __builtin_amdgcn_ballot_w64(act);
@@ -1323,7 +1335,7 @@ __global__ __launch_bounds__(kWave) void k_energy(DevGeom g, const float* __rest
             }
             S += __popcll(am);
         };
-        auto overflow = [&](unsigned long long mg) {
+        auto overflow = [&](unsigned long long mg, bool filter) {
             if constexpr (HS < NSLOT) {
                 unsigned long long ov = __builtin_amdgcn_ballot_w64(((mg >> (lane & 63)) & 1ull) && cur.cnt > HS);
                 while (ov) {
@@ -1340,12 +1352,13 @@ __global__ __launch_bounds__(kWave) void k_energy(DevGeom g, const float* __rest
                     const bool act = ee < nc && ps < c_cnt;
                     float ux = 0.0f, uy = 0.0f, uz = 0.0f;
                     if (act) {
-                        const float* row = disk + (int64_t)c_idx * 3 * nm;
-                        ux = row[ps] + isx;
-                        uy = row[nm + ps] + isy;
-                        uz = row[2 * nm + ps] + isz;
+                        using DA = DiskAddr<OFF32>;
+                        const uint32_t off = ((uint32_t)c_idx * (uint32_t)(3 * nm) + (uint32_t)ps) * DA::kUnit;
+                        ux = DA::ld(disk, off) + isx;
+                        uy = DA::ld(disk, off + (uint32_t)nm * DA::kUnit) + isy;
+                        uz = DA::ld(disk, off + 2u * (uint32_t)nm * DA::kUnit) + isz;
                     }
-                    put(act, ux, uy, uz);
+                    put(act && (!filter || near(ux, uy, uz)), ux, uy, uz);
                 }
             }
         };
@@ -1354,20 +1367,21 @@ __global__ __launch_bounds__(kWave) void k_energy(DevGeom g, const float* __rest
         // staged ranges: [0, n_own) own | main slots of the other cells in list order (weight-2
         // cells first: [n_own, A)) | overflow slots of weight-2 cells [B, C) | of weight-1 cells
         put(vact[0] && ee == 0, vx[0], vy[0], vz[0]);                 // own main slots
-        overflow(m0);                                                 // own slots [HS, n)
+        overflow(m0, false);                                          // own slots [HS, n)
         int A = S;
 #pragma unroll
         for (int q = 0; q < NPMAX; ++q) {
             const int e = q * CPP + ee;
             if (q * CPP < ncells) {
-                A += __popcll(__builtin_amdgcn_ballot_w64(vact[q] && e >= 1 && e < e0));
-                put(vact[q] && e >= 1, vx[q], vy[q], vz[q]);
+                const bool keep = vact[q] && e >= 1 && near(vx[q], vy[q], vz[q]);
+                A += __popcll(__builtin_amdgcn_ballot_w64(keep && e < e0));
+                put(keep, vx[q], vy[q], vz[q]);
             }
         }
         const int B = S;
-        overflow(m1);
+        overflow(m1, true);
         const int C2 = S;
-        overflow(m2);
+        overflow(m2, true);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         // ---- the next cell's rows go out now and arrive while this cell's pairs run
         if (c + 1 < ncl) {
@@ -1376,34 +1390,37 @@ __global__ __launch_bounds__(kWave) void k_energy(DevGeom g, const float* __rest
             if (c + 2 < ncl) nxt = energy_stencil(g, ncnt, t0 + (uint32_t)c + 2u);
         }
         if (n_own == 0) continue;
-        // ---- pairs (i, j): own particle i < n_own, staged j != i, flattened q = i*S + j (own-own
-        //      pairs in both directions, weight 1 each: bit-identical terms, like the oracle)
+        // ---- pairs (i, j): lane j holds staged partner j (blocks of 64), own particle i < n_own
+        //      (staged first: lane i of block 0) broadcast by readlane; j != i (own-own pairs in
+        //      both directions, weight 1 each: bit-identical terms, like the oracle)
         int head = 0, C = 0;   // ring: entries [head, head + C) mod 128
         auto drain = [&](int lim) {
             if (lane < lim) sum += energy_term(ring[(head + lane) & 127], r2min);
             head = (head + 64) & 127;
             C -= lim;
         };
-        const int total = n_own * S;
-        const float inv_s = 1.0f / (float)S;
-        for (int q0 = 0; q0 < total; q0 += kWave) {
-            const int q = q0 + lane;
-            int i = (int)((float)q * inv_s);                // q / S, corrected below (q < 2^13)
-            int j = q - i * S;
-            i = j < 0 ? i - 1 : (j >= S ? i + 1 : i);
-            j = q - i * S;
-            const bool valid = q < total && j != i;
-            const int ii = valid ? i : 0;
-            const int jj = valid ? j : 0;
-            const float xi = ex_[ii], yi = ey_[ii], zi = ez_[ii];
-            const float xj = ex_[jj], yj = ey_[jj], zj = ez_[jj];
-            const float r2 = pmc_r2(xi - xj, yi - yj, zi - zj);
-            const bool in = valid && r2 <= rc2;
+        const float ox = ex_[lane], oy = ey_[lane], oz = ez_[lane];   // block 0 (own at lanes < n_own)
+        for (int jb = 0; jb < S; jb += kWave) {
+            const int j = jb + lane;
+            const bool vj = j < S;
+            const int jj = vj ? j : 0;
+            const float xj = jb == 0 ? ox : ex_[jj], yj = jb == 0 ? oy : ey_[jj], zj = jb == 0 ? oz : ez_[jj];
             const bool w2 = (jj >= n_own && jj < A) || (jj >= B && jj < C2);
-            const unsigned long long im = __builtin_amdgcn_ballot_w64(in);
-            if (in) ring[(head + C + mbcnt64(im)) & 127] = w2 ? -r2 : r2;
-            C += __popcll(im);
-            if (C >= 64) drain(64);
+            const uint32_t sgn = w2 ? 0x80000000u : 0u;   // weight 2: listed with the sign bit set
+            const unsigned long long vm = __builtin_amdgcn_ballot_w64(vj);
+            for (int i = 0; i < n_own; ++i) {
+                const float xi = as_f(__builtin_amdgcn_readlane(as_i(ox), i));
+                const float yi = as_f(__builtin_amdgcn_readlane(as_i(oy), i));
+                const float zi = as_f(__builtin_amdgcn_readlane(as_i(oz), i));
+                const float r2 = pmc_r2(xi - xj, yi - yj, zi - zj);
+                // partners j < S, j != i (i is lane i of block 0), within the cutoff
+                const unsigned long long im = __builtin_amdgcn_ballot_w64(r2 <= rc2) & vm &
+                                              ~(jb == 0 ? 1ull << i : 0ull);
+                if (__builtin_amdgcn_inverse_ballot_w64(im))
+                    ring[(head + C + mbcnt64(im)) & 127] = as_f(as_i(r2) | (int)sgn);
+                C += __popcll(im);
+                if (C >= 64) drain(64);
+            }
         }
         if (C > 0) drain(C);
     }
@@ -1663,11 +1680,15 @@ hipError_t launch_energy(const DevGeom& g, const float* disk, const int16_t* n,
     const size_t lds = sizeof(float) * (3 * 27 * (size_t)g.nmax + 128 + 32);
     dim3 grid((unsigned)((total + kEnergyCells - 1) / kEnergyCells)), block(kWave);
     const uint32_t tc = (uint32_t)total;
+    // 32-bit byte offsets below 4 GiB of disk (every single-GPU 256^3 box), else element offsets
+    const int64_t bytes = (int64_t)g.cps_x * g.cps_y * (g.nz_local + 2 * g.halo) * 3 * g.nmax * 4;
+    const bool off32 = bytes < ((int64_t)1 << 32);
+    auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, block, lds, st, g, disk, n, acc, tc); };
     switch (g.nslot) {
-        case 8: hipLaunchKernelGGL(k_energy<8>, grid, block, lds, st, g, disk, n, acc, tc); break;
-        case 16: hipLaunchKernelGGL(k_energy<16>, grid, block, lds, st, g, disk, n, acc, tc); break;
-        case 32: hipLaunchKernelGGL(k_energy<32>, grid, block, lds, st, g, disk, n, acc, tc); break;
-        default: hipLaunchKernelGGL(k_energy<64>, grid, block, lds, st, g, disk, n, acc, tc); break;
+        case 8: off32 ? go(k_energy<8, true>) : go(k_energy<8, false>); break;
+        case 16: off32 ? go(k_energy<16, true>) : go(k_energy<16, false>); break;
+        case 32: off32 ? go(k_energy<32, true>) : go(k_energy<32, false>); break;
+        default: off32 ? go(k_energy<64, true>) : go(k_energy<64, false>); break;
     }
     return hipGetLastError();
 }
