@@ -28,3 +28,20 @@ def pmc():
     import pmc_amd
     pmc_amd.build()
     return pmc_amd
+
+
+@pytest.fixture(autouse=True)
+def _release_gpu_objects(request):
+    """GPU tests: contexts a test leaves behind are destroyed between tests (gc + device sync), not
+    at an arbitrary garbage-collection point inside the next test's GPU work."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    import gc
+    gc.collect()
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+    except ImportError:
+        pass
