@@ -1204,6 +1204,30 @@ int pmc_slab_init(pmc_ctx* c, int rank, int world, const unsigned char* id) {
         drop_slab(c);
         return rc;
     }
+    // Warm-up: one small message each way with both neighbours (the peers every exchange uses), then
+    // the whole device.  RCCL sets up peer connections lazily, with device allocations and work of
+    // its own; finishing that here keeps it from overlapping this process's later allocations and
+    // launches (a whole-box context created right after a one-rank RCCL slab has read back zero
+    // counts on a fresh box, intermittently).  Collective, like the communicator creation.
+    void* tmp = nullptr;
+    hipError_t e = hipMalloc(&tmp, 64);
+    if (e == hipSuccess) e = hipMemset(tmp, 0, 64);
+    if (e != hipSuccess) {
+        if (tmp) (void)hipFree(tmp);
+        drop_slab(c);
+        return hip_fail(e, "slab warm-up buffer");
+    }
+    xfer_send(s, (char*)tmp, 8, s->below);
+    xfer_send(s, (char*)tmp + 8, 8, s->above);
+    xfer_recv(s, (char*)tmp + 32, 8, s->above);
+    xfer_recv(s, (char*)tmp + 40, 8, s->below);
+    rc = xfer_run(s);
+    if (rc == PMC_OK && (e = hipDeviceSynchronize()) != hipSuccess) rc = hip_fail(e, "slab warm-up");
+    (void)hipFree(tmp);
+    if (rc) {
+        drop_slab(c);
+        return rc;
+    }
     return PMC_OK;
 }
 

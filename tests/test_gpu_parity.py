@@ -419,12 +419,15 @@ def test_gpu_c_slab_driver_equals_whole_box(pmc, oracle, nz, atoms, rccl):
     drv = SlabDriver(cps=16, nz_local=nz, rank=0, world=1, atoms_per_rank=atoms, use_rccl=rccl)
     whole = pmc.PmcContext(16, cps_z=nz)
     whole.init_lattice(atoms)
+    assert int(whole.copy_out()[1].sum()) == atoms, "whole box: lattice not binned"
     drv.run(10, 8)
     for s in range(10, 18):
         whole.sweep(s)
     torch.cuda.synchronize()
     d_slab, n_slab = drv.owned()
     disk, n = whole.copy_out()
+    assert int(n_slab.sum()) == atoms, "slab: particles lost"
+    assert int(n.sum()) == atoms, f"whole box: particles lost (sum {int(n.sum())}, stats {whole.stats()})"
     assert np.array_equal(n_slab, n)
     assert oracle.valid_slots_equal(d_slab, n_slab, disk, n, 16)
     d_all, n_all = drv.ctx.copy_out()
