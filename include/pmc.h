@@ -198,6 +198,12 @@ int pmc_slab_exchange(pmc_ctx* ctx);
 int pmc_slab_sweep(pmc_ctx* ctx, uint32_t sweep);
 /* Order the context stream after the outstanding exchanges (before reading state or halos). */
 int pmc_slab_finish(pmc_ctx* ctx);
+/* Observables of the whole box (one sum over the ranks per report): the four counters
+ * (pmc_stats_read without reset) and, with with_energy, the cell-list energy (pmc_energy), each
+ * summed over all ranks in fixed point -- exact, equal to a one-GPU run's -- through the slab's
+ * transport (one RCCL all-reduce, or the in-process group).  Collective: every rank calls it.
+ * Reference: kernel.cu:415 (accept_counter), kernel.cu:452-470 (calc_energy). */
+int pmc_slab_observables(pmc_ctx* ctx, int with_energy, pmc_stats* out, double* e_out);
 /* Sum of the HIP-event durations of the subsweep and shift launches since the last call
  * (synchronizes), then switch per-launch events on (enable = 1) or off.  The events ride on the
  * kernels' own dispatch packets (no extra packets between launches); graph replays and the

@@ -530,8 +530,9 @@ int pmc_run_graph(pmc_ctx* c, uint32_t first, int count) {
     return PMC_OK;
 }
 
-int pmc_energy(pmc_ctx* c, double* e_out) {
-    if (!c || !e_out) return fail(PMC_ERR_ARG, "bad argument");
+// sum over the context's owned cells of the fixed-point pair terms (k_energy; the energy is half of
+// it, scaled by 2^-32): exact, and exactly additive over slabs
+int energy_fixed(pmc_ctx* c, int64_t* fixed) {
     if (int rj = slab_join(c)) return rj;
     PMC_HIP(hipMemsetAsync(c->eacc, 0, sizeof(unsigned long long) * kStatSlots, c->stream));
     hipError_t e = launch_energy(c->G, c->disk[c->cur], c->n[c->cur], c->eacc, c->stream);
@@ -542,7 +543,15 @@ int pmc_energy(pmc_ctx* c, double* e_out) {
     PMC_HIP(hipStreamSynchronize(c->stream));
     unsigned long long s = 0;
     for (auto v : h) s += v;
-    *e_out = (double)(int64_t)s / PMC_FIX_SCALE * 0.5;
+    *fixed = (int64_t)s;
+    return PMC_OK;
+}
+
+int pmc_energy(pmc_ctx* c, double* e_out) {
+    if (!c || !e_out) return fail(PMC_ERR_ARG, "bad argument");
+    int64_t f = 0;
+    if (int rc = energy_fixed(c, &f)) return rc;
+    *e_out = (double)f / PMC_FIX_SCALE * 0.5;
     return PMC_OK;
 }
 
@@ -794,6 +803,7 @@ struct Rccl {
     decltype(&ncclGroupStart) group_start = nullptr;
     decltype(&ncclGroupEnd) group_end = nullptr;
     decltype(&ncclGetErrorString) error_string = nullptr;
+    decltype(&ncclAllReduce) all_reduce = nullptr;   // observables (pmc_slab_observables)
 };
 
 Rccl& rccl() {
@@ -815,6 +825,7 @@ Rccl& rccl() {
     r.group_start = (decltype(r.group_start))sym("ncclGroupStart");
     r.group_end = (decltype(r.group_end))sym("ncclGroupEnd");
     r.error_string = (decltype(r.error_string))sym("ncclGetErrorString");
+    r.all_reduce = (decltype(r.all_reduce))sym("ncclAllReduce");
     r.ok = r.get_unique_id && r.comm_init_rank && r.comm_destroy && r.send && r.recv && r.group_start &&
            r.group_end && r.error_string;
     if (!r.ok) r.err = "librccl lacks a required symbol";
@@ -855,6 +866,7 @@ struct pmc_local_group {
         hipEvent_t pulled = nullptr;   // ... after its receives (copies from the peers' buffers)
         std::vector<XferMsg> sends, recvs;
         bool joined = false;
+        uint64_t red[5] = {0, 0, 0, 0, 0};   // observables of the rank (pmc_slab_observables)
     };
     int world = 0;
     int timeout_ms = 120000;
@@ -1414,6 +1426,54 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
 int pmc_slab_finish(pmc_ctx* c) {
     if (!c || !c->slab) return fail(PMC_ERR_ARG, "no slab driver (pmc_slab_init)");
     return slab_join(c);
+}
+
+int pmc_slab_observables(pmc_ctx* c, int with_energy, pmc_stats* out, double* e_out) {
+    if (!c || !c->slab || !out || (with_energy && !e_out)) return fail(PMC_ERR_ARG, "bad argument");
+    pmc_slab* s = c->slab;
+    pmc_stats st;
+    if (int rc = pmc_stats_read(c, &st, 0)) return rc;
+    int64_t ef = 0;
+    if (with_energy)
+        if (int rc = energy_fixed(c, &ef)) return rc;
+    // two's-complement sums: exact for the signed fields as 64-bit unsigned sums
+    uint64_t v[5] = {(uint64_t)st.de_fixed, (uint64_t)st.accepted, (uint64_t)st.trials, (uint64_t)st.evaluated,
+                     (uint64_t)ef};
+    if (s->comm) {
+        Rccl& R = rccl();
+        if (!R.all_reduce) return fail(PMC_ERR_HIP, "librccl lacks ncclAllReduce");
+        void* d = nullptr;
+        PMC_HIP(hipMalloc(&d, sizeof v));
+        hipError_t e = hipMemcpy(d, v, sizeof v, hipMemcpyHostToDevice);
+        if (e != hipSuccess) { (void)hipFree(d); return hip_fail(e, "observables copy"); }
+        ncclResult_t r = R.all_reduce(d, d, 5, ncclUint64, ncclSum, s->comm, s->aux);
+        if (r != ncclSuccess) { (void)hipFree(d); return nccl_fail(r, "ncclAllReduce"); }
+        e = hipStreamSynchronize(s->aux);
+        if (e == hipSuccess) e = hipMemcpy(v, d, sizeof v, hipMemcpyDeviceToHost);
+        (void)hipFree(d);
+        if (e != hipSuccess) return hip_fail(e, "observables all-reduce");
+    } else if (s->group) {
+        pmc_local_group* g = s->group;
+        {
+            std::lock_guard<std::mutex> lk(g->m);
+            for (int k = 0; k < 5; ++k) g->slot[s->rank].red[k] = v[k];
+        }
+        if (int rc = group_barrier(g)) return rc;   // every rank's values are in
+        uint64_t t[5] = {0, 0, 0, 0, 0};
+        {
+            std::lock_guard<std::mutex> lk(g->m);
+            for (const auto& sl : g->slot)
+                for (int k = 0; k < 5; ++k) t[k] += sl.red[k];
+        }
+        if (int rc = group_barrier(g)) return rc;   // every rank has read them
+        for (int k = 0; k < 5; ++k) v[k] = t[k];
+    }
+    out->de_fixed = (int64_t)v[0];
+    out->accepted = (int64_t)v[1];
+    out->trials = (int64_t)v[2];
+    out->evaluated = (int64_t)v[3];
+    if (with_energy) *e_out = (double)(int64_t)v[4] / PMC_FIX_SCALE * 0.5;
+    return PMC_OK;
 }
 
 int pmc_timing_kinds(pmc_ctx* c, int enable, double ms[3], int count[3]) {

@@ -183,6 +183,16 @@ class PmcContext:
     def slab_finish(self) -> None:
         check("pmc_slab_finish", lib().pmc_slab_finish(self._h))
 
+    def slab_observables(self, with_energy: bool = True) -> tuple:
+        """Whole-box counters (and energy) summed over the ranks in fixed point, collectively
+        (pmc_slab_observables): (stats dict, energy or None)."""
+        st = Stats()
+        e = C.c_double(0.0)
+        check("pmc_slab_observables", lib().pmc_slab_observables(self._h, 1 if with_energy else 0, C.byref(st),
+                                                                 C.byref(e)))
+        d = {"de_fixed": st.de_fixed, "accepted": st.accepted, "trials": st.trials, "evaluated": st.evaluated}
+        return d, (e.value if with_energy else None)
+
     def _timing(self, fn: str, enable: bool) -> dict:
         a, b = C.c_double(), C.c_double()
         na, nb = C.c_int(), C.c_int()

@@ -74,7 +74,8 @@ def test_c_slab_driver_world_equals_oracle(pmc, oracle, world, cps, cps_y, cps_z
         drivers[r] = d
         d.run(first, count)
         d.ctx.synchronize()
-        return d.owned(), d.ctx.stats(), d.ctx.energy(), d.ctx.error_flags()
+        obs = d.ctx.slab_observables()          # collective: whole-box sums over the ranks
+        return d.owned(), d.ctx.stats(), d.ctx.energy(), d.ctx.error_flags(), obs
 
     res = _run_ranks(world, rank_main)
     st = oracle.OracleState(oracle.make_params(cps=cps, cps_y=cps_y, cps_z=cps_z))
@@ -83,7 +84,7 @@ def test_c_slab_driver_world_equals_oracle(pmc, oracle, world, cps, cps_y, cps_z
     plane, row = cps * cps_y, 3 * 16
     tot = {"de_fixed": 0, "accepted": 0, "trials": 0, "evaluated": 0}
     e_sum = 0.0
-    for r, ((d, n), s, e, fl) in enumerate(res):
+    for r, ((d, n), s, e, fl, _) in enumerate(res):
         ref = slice(r * nz * plane, (r + 1) * nz * plane)
         assert np.array_equal(n, st.n[ref]), f"rank {r}: counts differ"
         assert oracle.valid_slots_equal(d, n, st.disk[ref.start * row:ref.stop * row], st.n[ref], 16), \
@@ -95,6 +96,11 @@ def test_c_slab_driver_world_equals_oracle(pmc, oracle, world, cps, cps_y, cps_z
     assert tot == st.stats.as_dict()
     assert int(sum(int(n.sum()) for (_, n), *_ in res)) == atoms
     assert e_sum == pytest.approx(st.energy(), rel=1e-9, abs=1e-9)
+    # pmc_slab_observables: every rank gets the whole box's counters and its energy, summed in
+    # fixed point -- equal to the oracle's whole-box values exactly
+    for *_, (obs, e_all) in res:
+        assert obs == st.stats.as_dict()
+        assert e_all == st.energy()
     for d in drivers:
         d.ctx.close()
     group.close()

@@ -440,6 +440,8 @@ def test_gpu_c_slab_driver_equals_whole_box(pmc, oracle, nz, atoms, rccl):
     assert drv.ctx.stats() == whole.stats()
     assert drv.ctx.error_flags() == 0
     assert drv.ctx.energy() == pytest.approx(whole.energy(), rel=1e-12, abs=1e-9)
+    obs, e_all = drv.ctx.slab_observables()   # one rank: the RCCL all-reduce (or local) of itself
+    assert obs == whole.stats() and e_all == whole.energy()
 
 
 @pytest.mark.gpu
