@@ -1372,17 +1372,20 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
         int k1 = k;
         while (k1 < 8 && plan.order[k1] % 2 == q) ++k1;           // run [k, k1)
         const int p = 1 - q;                                      // parity of the previous run
+        // the sweep's first run needs no border waits: the previous sweep's shift joined every
+        // chain, and U and T wait for it (a stream wait costs a barrier packet on the critical path)
+        const bool first = k == 0;
         // L
-        if ((rc = border_waits(kL, 1, zs, q, S, p))) return rc;
+        if (!first && (rc = border_waits(kL, 1, zs, q, S, p))) return rc;
         if (zs > 1 && (rc = phases(S, c->ovf, 1, zs, k, k1, kL))) return rc;
         PMC_HIP(hipEventRecord(s->ev_run[kL][q], S));
         // U
-        if ((rc = border_waits(kU, zs, nz - 1, q, U, p))) return rc;
+        if (!first && (rc = border_waits(kU, zs, nz - 1, q, U, p))) return rc;
         if (nz - 1 > zs && (rc = phases(U, c->ovf_aux, zs, nz - 1, k, k1, kU))) return rc;
         PMC_HIP(hipEventRecord(s->ev_run[kU][q], U));
         // B, then the exchange
         const int zb = q == 0 ? 0 : nz - 1;
-        if ((rc = border_waits(kB, zb, zb + 1, q, T, p))) return rc;
+        if (!first && (rc = border_waits(kB, zb, zb + 1, q, T, p))) return rc;
         if ((rc = phases(T, c->ovf_b, zb, zb + 1, k, k1, kB))) return rc;
         PMC_HIP(hipEventRecord(s->ev_run[kB][q], T));
         if ((rc = slab_exchange_run(c, q))) return rc;
@@ -1408,16 +1411,11 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
     if (e != hipSuccess) return hip_fail(e, "shift launch");
     c->cur ^= 1;
     // U and T continue after the shift (it rewrote every plane); the z halo arrives on T, overlapping
-    // the next sweep's first interior launches (they read no halo)
-    // (the chains' "previous run" events all point at the shift: the next sweep's border waits then
-    // cost nothing -- in particular none waits for the z halo, which only B reads, in T order)
+    // the next sweep's first interior launches (they read no halo).  The next sweep's first run
+    // waits for nothing else (no border waits), so no "previous run" event is recorded here.
     PMC_HIP(hipEventRecord(s->ev_i, S));
     PMC_HIP(hipStreamWaitEvent(U, s->ev_i, 0));
     PMC_HIP(hipStreamWaitEvent(T, s->ev_i, 0));
-    for (int j = 0; j < 3; ++j) {
-        PMC_HIP(hipEventRecord(s->ev_run[j][0], S));
-        PMC_HIP(hipEventRecord(s->ev_run[j][1], S));
-    }
     if (dir != 0 && (rc = slab_exchange_zplane(c, dir))) return rc;
     PMC_HIP(hipEventRecord(s->ev_x, T));
     return PMC_OK;
