@@ -51,6 +51,11 @@ for rep in range(2):
         print(f"  {nm:14s} mean {d[:, k].mean():8.0f}  median {np.median(d[:, k]):8.0f}  "
               f"share {d[:, k].mean() / life.mean() * 100:5.1f}%")
     print(f"  lifetime mean {life.mean():.0f} median {np.median(life):.0f} p99 {np.percentile(life, 99):.0f}")
+    # two cells per wave: cell A = even colour-cell index, B = odd (B's loads go out after A's visit)
+    idx = np.nonzero(full)[0]
+    for nm_ab, sel in (("A (even)", idx % 2 == 0), ("B (odd)", idx % 2 == 1)):
+        dd = d[sel]
+        print(f"  cell {nm_ab}: " + ", ".join(f"{nm} {dd[:, k].mean():.0f}" for k, nm in enumerate(names)))
     starts = np.sort(st[full, 0].astype(np.int64) - base)
     print(f"  start quantiles (ticks): " + " ".join(f"{q}%:{np.percentile(starts, q):.0f}" for q in (1, 10, 50, 90, 99)))
     ends = np.sort(st[full, 9].astype(np.int64) - base)
