@@ -227,22 +227,45 @@ __device__ __forceinline__ int64_t sidx(const DevGeom& g, int x, int y, int zl) 
 // entries from kOvfHead.  Zero between launches (the fallback's last workgroup resets it).
 constexpr int kOvfCount = 0, kOvfDone = 1;
 
-// Wave-uniform geometry of one cell visit: t -> (ta, tb, tc) by host-computed magic division
-// (SALU only), the cell's storage index, its global id (the RNG counter) and whether its stencil
-// crosses a box face.
+// Visiting order of the main launch (speed only: cells of a colour are independent).  Colour cell
+// index t = ta + hx*(tb + hy*tc) (the stats slot and the overflow queue's entry); the main launch
+// visits position p in groups of PMC_ZGROUP colour planes: x fastest, then the planes of the group,
+// then y, then the group (cell_geo with zlog = log2 PMC_ZGROUP).  A stencil row of a
+// plane between two colour planes is read by both of them; with x, y, z order those reads lie a
+// whole colour plane of cells apart (more than an XCD's L2 holds), within a group they lie one row
+// of cells apart.  With the XCD-aware block order an XCD's contiguous range is whole groups (at
+// 128^3: 64 colour planes, 16 groups of 4, two per XCD).  Fabric reads per launch at 128^3/1e7:
+// 835 MB in plain order, 497 MB in groups of 4; phase -0.5..1%, 256^3 box -2.3%; groups of 16
+// were 15% slower at the same traffic (profiles/r02x_zgroup_ab.txt).  Ranges whose plane count
+// PMC_ZGROUP does not divide keep the plain order.
+#ifndef PMC_ZGROUP
+#define PMC_ZGROUP 4
+#endif
+constexpr int ilog2_exact(int v) { return v <= 1 ? 0 : 1 + ilog2_exact(v >> 1); }
+static_assert((PMC_ZGROUP & (PMC_ZGROUP - 1)) == 0, "PMC_ZGROUP must be a power of two");
+constexpr int kZGroupLog = ilog2_exact(PMC_ZGROUP);
+
+// Wave-uniform geometry of one cell visit: position p -> (ta, tb, tc) by host-computed magic
+// division (SALU only; zlog = 0: the plain order, p = t), the colour cell index t, the cell's
+// storage index, its global id (the RNG counter) and whether its stencil crosses a box face.
 struct CellGeo {
-    int ta, tb, x, y, zl, zg0;
+    int t, ta, tb, x, y, zl, zg0;
     uint32_t c, id;
     bool edge;
 };
 
-__device__ __forceinline__ CellGeo cell_geo(const DevGeom& g, int t, int cz0, int ox, int oy, int oz) {
+__device__ __forceinline__ CellGeo cell_geo(const DevGeom& g, int p, int cz0, int ox, int oy, int oz,
+                                            int zlog = 0) {
     CellGeo cg;
-    const uint32_t q1 = udiv_magic((uint32_t)t, g.div_ncx);
-    const uint32_t q2 = udiv_magic(q1, g.div_ncy);
-    cg.ta = t - (int)q1 * (g.cps_x >> 1);
-    cg.tb = (int)q1 - (int)q2 * (g.cps_y >> 1);
-    const int tc = cz0 + (int)q2;                          // colour plane (z = 2*tc + oz)
+    const int hx = g.cps_x >> 1, hy = g.cps_y >> 1;
+    const uint32_t q1 = udiv_magic((uint32_t)p, g.div_ncx);     // p / hx
+    const uint32_t q3 = q1 >> zlog;
+    const uint32_t q2 = udiv_magic(q3, g.div_ncy);               // group (plain order: plane)
+    cg.ta = p - (int)q1 * hx;
+    cg.tb = (int)q3 - (int)q2 * hy;
+    const int tcr = ((int)q2 << zlog) + (int)(q1 & ((1u << zlog) - 1u));   // colour plane in the range
+    cg.t = zlog ? cg.ta + hx * (cg.tb + hy * tcr) : p;
+    const int tc = cz0 + tcr;                              // colour plane (z = 2*tc + oz)
     cg.x = 2 * cg.ta + ox;
     cg.y = 2 * cg.tb + oy;
     cg.zl = 2 * tc + oz;
@@ -763,8 +786,8 @@ template <int NSLOT, int NMC, int LCAP, bool OFF32, bool MIRROR = false>
 __device__ __forceinline__ void subsweep_pair(const DevGeom& g, float* __restrict__ disk,
                                               const int16_t* __restrict__ ncnt, int ox, int oy, int oz,
                                               uint32_t sweep, unsigned long long* __restrict__ stats,
-                                              float* __restrict__ px_, int lcap_rt, int cap, int tA, bool hasB,
-                                              int cz0, int* __restrict__ ovf, float* __restrict__ mirror = nullptr,
+                                              float* __restrict__ px_, int lcap_rt, int cap, int pA, int pB, bool hasB,
+                                              int cz0, int zlog, int* __restrict__ ovf, float* __restrict__ mirror = nullptr,
                                               int mirror_mode = 0) {
     const int lane = threadIdx.x & (kWave - 1);
     const int nm = NMC > 0 ? NMC : g.nmax;
@@ -776,10 +799,11 @@ __device__ __forceinline__ void subsweep_pair(const DevGeom& g, float* __restric
     float* buf = pz_ + stride;
     const int h = lane & 32;                       // 0: cell A's half, 32: cell B's
     const int l = lane & 31;
+    const CellGeo ca = cell_geo(g, pA, cz0, ox, oy, oz, zlog);
+    const CellGeo cb = cell_geo(g, hasB ? pB : pA, cz0, ox, oy, oz, zlog);
+    const int tA = ca.t, tB = cb.t;
     [[maybe_unused]] int t = tA;                   // (PMC_STAMP's cell index)
     PMC_STAMP(0);
-    const CellGeo ca = cell_geo(g, tA, cz0, ox, oy, oz);
-    const CellGeo cb = cell_geo(g, hasB ? tA + 1 : tA, cz0, ox, oy, oz);
     // ---- stencil tables of both cells, counts ----------------------------------------------
     CellGeo cl = ca;                               // this lane's cell (per-lane selects)
     cl.x = h ? cb.x : ca.x;
@@ -837,18 +861,19 @@ __device__ __forceinline__ void subsweep_pair(const DevGeom& g, float* __restric
         if (lane == 0 && ovf) ovf[kOvfHead + atomicAdd(&ovf[kOvfCount], 1)] = tA;
     }
     if (!hasB) return;
-    t = tA + 1;
+    t = tB;
     PMC_STAMP(0);
     PMC_STAMP(1);
     park(32);
     ld.issue(g, disk, cb, k_off, 32);
     PMC_STAMP(2);
     PMC_STAMP(3);
-    if (!visit_cell<NSLOT, NMC, LCAP, OFF32, MIRROR>(g, disk, sweep, stats, px_, lcap, cap, tA + 1, cb, 32, k_cnt,
+    if (!visit_cell<NSLOT, NMC, LCAP, OFF32, MIRROR>(g, disk, sweep, stats, px_, lcap, cap, tB, cb, 32, k_cnt,
                                                      k_off, sl.sx, sl.sy, sl.sz, ld, jv, 16, 10, mirror, mirror_mode)) {
-        if (lane == 0 && ovf) ovf[kOvfHead + atomicAdd(&ovf[kOvfCount], 1)] = tA + 1;
+        if (lane == 0 && ovf) ovf[kOvfHead + atomicAdd(&ovf[kOvfCount], 1)] = tB;
     }
 }
+
 
 
 // Main launch: one wave per cell of the colour; LDS layout for kMainCap partners, capacity `cap`
@@ -872,11 +897,13 @@ __global__ __launch_bounds__(kWave * kSubWaves) __attribute__((amdgpu_waves_per_
 #endif
     const int total = (g.cps_x >> 1) * (g.cps_y >> 1) * ncz;
 #if PMC_CELLS_PER_WAVE == 2
-    // two cells per wave (shared stencil table and RNG pass): wave w takes cells 2w and 2w+1
+    // two cells per wave (shared stencil table and RNG pass): wave w takes the cells at positions
+    // 2w and 2w+1 of the visiting order
     const int t = 2 * ((int)b * kSubWaves + wv);
     if (t >= total) return;
-    subsweep_pair<NSLOT, NMC, kMainCap, OFF32>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, kMainCap, cap, t,
-                                               t + 1 < total, cz0, ovf);
+    const int zlog = (ncz & ((1 << kZGroupLog) - 1)) == 0 ? kZGroupLog : 0;
+    subsweep_pair<NSLOT, NMC, kMainCap, OFF32>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, kMainCap, cap, t, t + 1,
+                                               t + 1 < total, cz0, zlog, ovf);
 #else
     const int t = (int)b * kSubWaves + wv;
     if (t >= total) return;
