@@ -1418,8 +1418,9 @@ __global__ __launch_bounds__(kWave) void k_energy(DevGeom g, const float* __rest
         }
         if (n_own == 0) continue;
         // ---- pairs (i, j): lane j holds staged partner j (blocks of 64), own particle i < n_own
-        //      (staged first: lane i of block 0) broadcast by readlane; j != i (own-own pairs in
-        //      both directions, weight 1 each: bit-identical terms, like the oracle)
+        //      (staged first: lane i of block 0) broadcast by readlane.  Own-own pairs once, j > i,
+        //      weight 2: r2(xi - xj) and r2(xj - xi) are the same bits (the oracle's two directed
+        //      terms, weight 1 each, sum to the same fixed-point value)
         int head = 0, C = 0;   // ring: entries [head, head + C) mod 128
         auto drain = [&](int lim) {
             if (lane < lim) sum += energy_term(ring[(head + lane) & 127], r2min);
@@ -1427,28 +1428,37 @@ __global__ __launch_bounds__(kWave) void k_energy(DevGeom g, const float* __rest
             C -= lim;
         };
         const float ox = ex_[lane], oy = ey_[lane], oz = ez_[lane];   // block 0 (own at lanes < n_own)
-        for (int jb = 0; jb < S; jb += kWave) {
+        auto block = [&](int jb, auto first_c) {
+            constexpr bool kFirst = decltype(first_c)::value;
             const int j = jb + lane;
             const bool vj = j < S;
             const int jj = vj ? j : 0;
-            const float xj = jb == 0 ? ox : ex_[jj], yj = jb == 0 ? oy : ey_[jj], zj = jb == 0 ? oz : ez_[jj];
-            const bool w2 = (jj >= n_own && jj < A) || (jj >= B && jj < C2);
-            const uint32_t sgn = w2 ? 0x80000000u : 0u;   // weight 2: listed with the sign bit set
-            const unsigned long long vm = __builtin_amdgcn_ballot_w64(vj);
+            float xj = ox, yj = oy, zj = oz;
+            if constexpr (!kFirst) {
+                xj = ex_[jj];
+                yj = ey_[jj];
+                zj = ez_[jj];
+            }
+            const bool w2 = jj < A || (jj >= B && jj < C2);   // own (j > i), mutual forward
+            const uint32_t sgn = w2 ? 0x80000000u : 0u;       // weight 2: listed with the sign bit set
+            // partners j < S; in block 0 the lanes j > i (lanes 0..n_own-1 are all valid, so
+            // clearing the lowest set bit each step drops lane i)
+            unsigned long long vm = __builtin_amdgcn_ballot_w64(vj);
             for (int i = 0; i < n_own; ++i) {
                 const float xi = as_f(__builtin_amdgcn_readlane(as_i(ox), i));
                 const float yi = as_f(__builtin_amdgcn_readlane(as_i(oy), i));
                 const float zi = as_f(__builtin_amdgcn_readlane(as_i(oz), i));
                 const float r2 = pmc_r2(xi - xj, yi - yj, zi - zj);
-                // partners j < S, j != i (i is lane i of block 0), within the cutoff
-                const unsigned long long im = __builtin_amdgcn_ballot_w64(r2 <= rc2) & vm &
-                                              ~(jb == 0 ? 1ull << i : 0ull);
+                if constexpr (kFirst) vm &= vm - 1ull;
+                const unsigned long long im = __builtin_amdgcn_ballot_w64(r2 <= rc2) & vm;
                 if (__builtin_amdgcn_inverse_ballot_w64(im))
                     ring[(head + C + mbcnt64(im)) & 127] = as_f(as_i(r2) | (int)sgn);
                 C += __popcll(im);
                 if (C >= 64) drain(64);
             }
-        }
+        };
+        block(0, std::true_type{});
+        for (int jb = kWave; jb < S; jb += kWave) block(jb, std::false_type{});
         if (C > 0) drain(C);
     }
     // wave sum (int64, exact in any order), one atomic per wave
