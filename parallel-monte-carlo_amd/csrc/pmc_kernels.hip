@@ -1207,8 +1207,29 @@ struct EnergyStencil {
     int x, y, zg;      // the cell (wave-uniform): its box filters the staged partners
 };
 
+// Per-lane constants of the stencil (lane k < 27): the storage offset of neighbour k from its cell
+// (periodic wrap aside) and the group of an interior cell's neighbour k (0 own, 1 forward, 3
+// backward; lanes >= 27: 3).  Computed once per wave.
+struct EnergyLaneConst {
+    int dk;
+    int grp_in;
+};
+
+__device__ __forceinline__ EnergyLaneConst energy_lane_const(const DevGeom& g) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int k = lane < 27 ? lane : 0;
+    const int dx = (int)bit_of(kStencilPos[0], k) - (int)bit_of(kStencilNeg[0], k);
+    const int dy = (int)bit_of(kStencilPos[1], k) - (int)bit_of(kStencilNeg[1], k);
+    const int dz = (int)bit_of(kStencilPos[2], k) - (int)bit_of(kStencilNeg[2], k);
+    const bool forward = dz > 0 || (dz == 0 && (dy > 0 || (dy == 0 && dx > 0)));
+    EnergyLaneConst lc;
+    lc.dk = dx + g.cps_x * (dy + g.cps_y * dz);
+    lc.grp_in = lane >= 27 ? 3 : (k == 0 ? 0 : (forward ? 1 : 3));
+    return lc;
+}
+
 __device__ __forceinline__ EnergyStencil energy_stencil(const DevGeom& g, const int16_t* __restrict__ ncnt,
-                                                        uint32_t t) {
+                                                        uint32_t t, const EnergyLaneConst& lc) {
     const int lane = threadIdx.x & (kWave - 1);
     // t is wave-uniform: scalar magic division (host-computed divisors)
     const uint32_t q1 = udiv_magic(t, g.div_cx);          // t / cps_x
@@ -1216,15 +1237,25 @@ __device__ __forceinline__ EnergyStencil energy_stencil(const DevGeom& g, const 
     const int x = (int)(t - q1 * (uint32_t)g.cps_x);
     const int zl = (int)zq;
     const int y = (int)(q1 - zq * (uint32_t)g.cps_y);
+    EnergyStencil e;
+    e.x = x;
+    e.y = y;
+    e.zg = g.z0 + zl;
+    // interior cell (no neighbour wrapped or in a halo plane): every neighbour is mutual, the
+    // storage cells are plain offsets (same values as the general path below)
+    if (x >= 1 && x <= g.cps_x - 2 && y >= 1 && y <= g.cps_y - 2 && zl >= 1 && zl <= g.nz_local - 2 &&
+        e.zg >= 1 && e.zg <= g.cps_z - 2) {
+        e.kc = (int)t + g.cps_x * g.cps_y * g.halo + lc.dk;
+        e.sx = e.sy = e.sz = 0.0f;
+        e.grp = lc.grp_in;
+        e.cnt = e.grp < 3 ? (int)ncnt[e.kc] : 0;
+        return e;
+    }
     const int k = lane < 27 ? lane : 0;
     // lane k = 9*hx + 3*hy + hz, h = 0, 1, 2 -> offset 0, -1, +1 (the subsweep's stencil masks)
     const int dx = (int)bit_of(kStencilPos[0], k) - (int)bit_of(kStencilNeg[0], k);
     const int dy = (int)bit_of(kStencilPos[1], k) - (int)bit_of(kStencilNeg[1], k);
     const int dz = (int)bit_of(kStencilPos[2], k) - (int)bit_of(kStencilNeg[2], k);
-    EnergyStencil e;
-    e.x = x;
-    e.y = y;
-    e.zg = g.z0 + zl;
     // periodic wrap as selects, 32-bit storage index (< 2^31 storage cells, normalise)
     const int nx0 = x + dx, ny0 = y + dy, zg = g.z0 + zl + dz, nz0 = zl + dz;
     const int nx = nx0 + (nx0 < 0 ? g.cps_x : 0) - (nx0 >= g.cps_x ? g.cps_x : 0);
@@ -1338,10 +1369,11 @@ __global__ __launch_bounds__(kWave) void k_energy(DevGeom g, const float* __rest
         }
     };
 
-    EnergyStencil cur = energy_stencil(g, ncnt, t0);
+    const EnergyLaneConst lc = energy_lane_const(g);
+    EnergyStencil cur = energy_stencil(g, ncnt, t0, lc);
     issue_rows(cur);
     EnergyStencil nxt = cur;
-    if (ncl > 1) nxt = energy_stencil(g, ncnt, t0 + 1);
+    if (ncl > 1) nxt = energy_stencil(g, ncnt, t0 + 1, lc);
     for (int c = 0; c < ncl; ++c) {
         // ---- stage cell c from the rows in registers: own cell (all slots), weight-2 cells,
         //      then weight-1 cells (each group: main slots, then the fuller cells' slots [HS, n))
@@ -1414,7 +1446,7 @@ __global__ __launch_bounds__(kWave) void k_energy(DevGeom g, const float* __rest
         if (c + 1 < ncl) {
             cur = nxt;
             issue_rows(cur);
-            if (c + 2 < ncl) nxt = energy_stencil(g, ncnt, t0 + (uint32_t)c + 2u);
+            if (c + 2 < ncl) nxt = energy_stencil(g, ncnt, t0 + (uint32_t)c + 2u, lc);
         }
         if (n_own == 0) continue;
         // ---- pairs (i, j): lane j holds staged partner j (blocks of 64), own particle i < n_own
