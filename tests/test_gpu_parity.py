@@ -475,3 +475,46 @@ def test_gpu_c_slab_driver_timing_and_restart(pmc, oracle, tmp_path):
     assert np.array_equal(n1, n2)
     assert oracle.valid_slots_equal(d1, n1, d2, n2, 16)
     assert drv2.ctx.stats() == s1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("slab,rccl", [(False, False), (True, False), (True, True)])
+def test_bench_rewarm_restores_state(pmc, oracle, slab, rccl):
+    """bench.py's clock re-warm (hot-path sweeps on the timed start state, then device-to-device
+    restore) leaves the run bit-identical to one without it: every occupied slot, counts, the
+    counters of the following sweeps and the energy; for the slab driver the other streams are
+    ordered after the save and the restore copies (a torn save broke the ΔE bookkeeping once)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from pmc_amd.slab import SlabDriver
+
+    def make():
+        if not slab:
+            c = pmc.PmcContext(16)
+            c.init_lattice(10_000)
+            return c, c.sweep, (lambda: None), (lambda: c.copy_out()), None
+        d = SlabDriver(cps=16, nz_local=16, rank=0, world=1, atoms_per_rank=10_000, use_rccl=rccl)
+        return d.ctx, d.sweep, d.finish, d.owned, (lambda: d.ctx.slab_exchange())
+
+    res = []
+    for use in (False, True):
+        ctx, sweep, finish, state, relink = make()
+        for s in range(3):
+            sweep(s)
+        finish()
+        ctx.synchronize()
+        ctx.stats(reset=True)
+        if use:
+            bench.rewarm(ctx, sweep, finish, first=3, count=3, relink=relink)
+        for s in range(3, 6):
+            sweep(s)
+        finish()
+        ctx.synchronize()
+        d, n = state()
+        res.append((d, n, ctx.stats(), ctx.energy(), ctx.error_flags()))
+    (d0, n0, s0, e0, f0), (d1, n1, s1, e1, f1) = res
+    assert np.array_equal(n0, n1)
+    assert oracle.valid_slots_equal(d0, n0, d1, n1, 16)
+    assert s0 == s1 and e0 == e1 and f0 == f1 == 0

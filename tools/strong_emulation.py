@@ -33,6 +33,10 @@ def main() -> int:
     ap.add_argument("--atoms", type=int, default=10_000_000)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warm-ms", type=float, default=80.0,
+                    help="keep warming up (more sweeps) until this much time has passed: an idle "
+                         "MI355X needs ~25 ms of this workload to reach its steady clock")
+    ap.add_argument("--rank-steps", type=int, default=100, help="timed sweeps of the emulated rank")
     ap.add_argument("--p2p", choices=["rccl", "local"], default="rccl")
     ap.add_argument("--driver", choices=["c", "python"], default="c",
                     help="c: the C slab driver (pmc_slab_*, product); python: SlabSimulation")
@@ -60,13 +64,17 @@ def main() -> int:
             full.phase(colour, s)
         full.shift(s)
 
-    for s in range(args.warmup):
-        full_sweep(s)
+    w0, t_w = 0, time.perf_counter()
+    while w0 < args.warmup or (time.perf_counter() - t_w) * 1e3 < args.warm_ms:
+        full_sweep(w0)
+        w0 += 1
+        if w0 % 8 == 0:
+            full.synchronize()
     full.synchronize()
     full.stats(reset=True)
     t0 = time.perf_counter()
     for k in range(args.steps):
-        full_sweep(args.warmup + k)
+        full_sweep(w0 + k)
     full.synchronize()
     t1 = (time.perf_counter() - t0) / args.steps
     trials_full = full.stats()["trials"] / args.steps
@@ -99,27 +107,32 @@ def main() -> int:
         from pmc_amd.slab import SlabDriver
         sim = SlabDriver(cps=cps, nz_local=nz, rank=0, world=1, stream=stream, use_rccl=args.p2p == "rccl")
         sim.load_state(d, n)
-    for s in range(args.warmup):
-        sim.sweep(s)
+    w1, t_w = 0, time.perf_counter()
+    while w1 < args.warmup or (time.perf_counter() - t_w) * 1e3 < args.warm_ms:
+        sim.sweep(w1)
+        w1 += 1
+        if w1 % 32 == 0:
+            sim.finish()
+            torch.cuda.synchronize()
     sim.finish()
     torch.cuda.synchronize()
     sim.ctx.stats(reset=True)
     t0 = time.perf_counter()
     issue = 0.0
-    for k in range(args.steps):
+    for k in range(args.rank_steps):
         ti = time.perf_counter()
-        sim.sweep(args.warmup + k)
+        sim.sweep(w1 + k)
         issue += time.perf_counter() - ti
     sim.finish()
     torch.cuda.synchronize()
-    tr = (time.perf_counter() - t0) / args.steps
-    trials_rank = sim.ctx.stats()["trials"] / args.steps
+    tr = (time.perf_counter() - t0) / args.rank_steps
+    trials_rank = sim.ctx.stats()["trials"] / args.rank_steps
     # the same sweeps issued with the GPU idle-free: host time per sweep when it never waits
     with torch.cuda.stream(stream):
         torch.cuda._sleep(int(2e9))      # ~1 s of GPU spin so the host runs ahead unblocked
     ti = time.perf_counter()
     for k in range(3):
-        sim.sweep(args.warmup + args.steps + k)
+        sim.sweep(w1 + args.rank_steps + k)
     host_only = (time.perf_counter() - ti) / 3
     sim.finish()
     torch.cuda.synchronize()
@@ -130,7 +143,7 @@ def main() -> int:
            "rank_sweep_ms": tr * 1e3, "rank_trial_moves_per_s": trials_rank / tr,
            "projected_speedup": t1 / tr, "projected_efficiency": t1 / tr / R,
            "projected_whole_job_trial_moves_per_s": trials_rank * R / tr,
-           "host_issue_ms_per_sweep": issue / args.steps * 1e3, "host_only_ms_per_sweep": host_only * 1e3,
+           "host_issue_ms_per_sweep": issue / args.rank_steps * 1e3, "host_only_ms_per_sweep": host_only * 1e3,
            "error_flags": flags,
            "note": "one GPU running one rank's slab of the config-4 box with the product slab driver; "
                    "excludes xGMI link time and neighbour skew"}
