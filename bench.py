@@ -272,6 +272,9 @@ def main() -> int:
                     help="sweeps run on the timed start state right before the timed region, which is "
                          "then restored on the device (the GPU comes out of the host analysis idle "
                          "and needs ~10 sweeps to reach its steady clock; 0: off)")
+    ap.add_argument("--timing-every", type=int, default=4,
+                    help="per-launch HIP events on the launches of every k-th timed sweep (the roofline's "
+                         "kernel times; events on every launch cost ~1.3%% of the sweep)")
     ap.add_argument("--slab", action="store_true", help="config 3 through the z-slab driver with one rank")
     ap.add_argument("--self-rccl", action="store_true",
                     help="one slab rank: halos through a one-rank RCCL communicator (default for config 5)")
@@ -395,7 +398,11 @@ def main() -> int:
     if args.graph and not slab:
         sim.run_graph(first, args.steps)
     else:
+        timed = not args.no_events
+        every = max(1, args.timing_every)
         for k in range(args.steps):
+            if timed and every > 1:
+                sim.timing_pause(k % every != 0)   # events on sweeps 0, every, 2*every, ...
             one_sweep(first + k)
         finish()
     torch.cuda.synchronize()

@@ -214,6 +214,10 @@ int pmc_slab_observables(pmc_ctx* ctx, int with_energy, pmc_stats* out, double* 
  * boundary planes, which run concurrently with [0]: their durations overlap and do not add). */
 int pmc_timing(pmc_ctx* ctx, int enable, double* subsweep_ms, int* n_subsweep, double* shift_ms, int* n_shift);
 int pmc_timing_kinds(pmc_ctx* ctx, int enable, double ms[3], int count[3]);
+/* Pause (paused = 1) or resume the per-launch events of pmc_timing without collecting them (no
+ * synchronization): a caller times a sample of its launches, e.g. every k-th sweep, and the events'
+ * own cost (about 1.3% of a sweep when every launch carries them) shrinks with the sample. */
+int pmc_timing_pause(pmc_ctx* ctx, int paused);
 int pmc_slab_timing(pmc_ctx* ctx, int enable, double* subsweep_ms, int* n_subsweep, double* shift_ms,
                     int* n_shift);
 /* The per-sweep plan every rank replicates (no broadcast): colour order (FY_Shuffle + itoa,

@@ -47,6 +47,7 @@ struct pmc_ctx {
     hipGraphExec_t graph_exec = nullptr;
     // per-launch kernel timing (pmc_timing): dispatch-packet events, (start, stop) pairs in use
     bool timing = false;
+    bool timing_paused = false;           // pmc_timing_pause: events off without collecting
     std::vector<hipEvent_t> tev;
     std::vector<int> tkind;                // 0 subsweep (context stream), 1 shift, 2 subsweep (aux stream)
     uint32_t graph_first = 0;
@@ -159,7 +160,7 @@ int slab_join(pmc_ctx* c);   // slab driver streams -> context stream (defined w
 // the next timing slot when pmc_timing is on (nullptr otherwise): events ride on the launch's
 // dispatch packet (hipExtLaunchKernelGGL), no extra packets in the stream
 const LaunchTiming* next_timing(pmc_ctx* c, int kind, LaunchTiming* lt) {
-    if (!c->timing) return nullptr;
+    if (!c->timing || c->timing_paused) return nullptr;
     const size_t k = c->tkind.size();
     while (c->tev.size() < 2 * (k + 1)) {
         hipEvent_t e;
@@ -1495,6 +1496,13 @@ int pmc_timing_kinds(pmc_ctx* c, int enable, double ms[3], int count[3]) {
     }
     c->tkind.clear();
     c->timing = enable != 0;
+    c->timing_paused = false;
+    return PMC_OK;
+}
+
+int pmc_timing_pause(pmc_ctx* c, int paused) {
+    if (!c) return fail(PMC_ERR_ARG, "null ctx");
+    c->timing_paused = paused != 0;
     return PMC_OK;
 }
 

@@ -212,6 +212,10 @@ class PmcContext:
         return {"subsweep_ms": ms[0], "n_subsweep": cnt[0], "shift_ms": ms[1], "n_shift": cnt[1],
                 "boundary_ms": ms[2], "n_boundary": cnt[2]}
 
+    def timing_pause(self, paused: bool) -> None:
+        """Per-launch events off (paused) or back on without collecting them (pmc_timing_pause)."""
+        check("pmc_timing_pause", lib().pmc_timing_pause(self._h, int(paused)))
+
     def slab_timing(self, enable: bool) -> dict:
         return self._timing("pmc_slab_timing", enable)
 
