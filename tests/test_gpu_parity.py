@@ -518,3 +518,21 @@ def test_bench_rewarm_restores_state(pmc, oracle, slab, rccl):
     assert np.array_equal(n0, n1)
     assert oracle.valid_slots_equal(d0, n0, d1, n1, 16)
     assert s0 == s1 and e0 == e1 and f0 == f1 == 0
+
+
+@pytest.mark.gpu
+def test_timing_pause_samples_launches(pmc):
+    """pmc_timing_pause: launches issued while paused carry no events and are not counted; the
+    collected sums cover exactly the unpaused sweeps (bench.py times every 4th sweep this way)."""
+    ctx = pmc.PmcContext(16)
+    ctx.init_lattice(10_000)
+    ctx.timing_kinds(True)
+    for s in range(4):
+        ctx.timing_pause(s % 2 == 1)
+        ctx.sweep(s)
+    k = ctx.timing_kinds(False)
+    assert k["n_subsweep"] == 2 * 8 and k["n_shift"] == 2 and k["subsweep_ms"] > 0
+    ctx.timing_kinds(True)      # a new collection starts unpaused
+    ctx.sweep(4)
+    k = ctx.timing_kinds(False)
+    assert k["n_subsweep"] == 8 and k["n_shift"] == 1
