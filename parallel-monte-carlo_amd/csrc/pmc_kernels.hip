@@ -1298,7 +1298,16 @@ __device__ __forceinline__ int64_t energy_term(float r2s, float r2min) {
 // order, so the total equals the oracle's bit for bit.  The next cell's rows are loaded while
 // the current cell's pairs run (the kernel is otherwise latency-bound: two dependent HBM round
 // trips per cell).
-constexpr int kEnergyCells = 8;
+#ifndef PMC_ENERGY_CELLS
+#define PMC_ENERGY_CELLS 16
+#endif
+constexpr int kEnergyCells = PMC_ENERGY_CELLS;
+// own particles per pair-loop step (1 or 2: two broadcast particles share the loop control, the
+// ring accounting and the drain test)
+#ifndef PMC_ENERGY_STEP
+#define PMC_ENERGY_STEP 1
+#endif
+constexpr int kEnergyRing = PMC_ENERGY_STEP == 2 ? 256 : 128;
 
 template <int NSLOT, bool OFF32>
 __global__ __launch_bounds__(kWave) void k_energy(DevGeom g, const float* __restrict__ disk,
@@ -1314,8 +1323,8 @@ __global__ __launch_bounds__(kWave) void k_energy(DevGeom g, const float* __rest
     float* ex_ = esm;
     float* ey_ = esm + cap;
     float* ez_ = esm + 2 * cap;
-    float* ring = esm + 3 * cap;                      // 128-entry ring of listed pairs (signed r2)
-    int* inv_l = (int*)(ring + 128);                  // list entry -> stencil lane (32 ints)
+    float* ring = esm + 3 * cap;                      // ring of listed pairs (signed r2)
+    int* inv_l = (int*)(ring + kEnergyRing);          // list entry -> stencil lane (32 ints)
     const int p = lane % HS;
     const int ee = lane / HS;
     const float rc2 = g.rc2;
@@ -1453,10 +1462,11 @@ __global__ __launch_bounds__(kWave) void k_energy(DevGeom g, const float* __rest
         //      (staged first: lane i of block 0) broadcast by readlane.  Own-own pairs once, j > i,
         //      weight 2: r2(xi - xj) and r2(xj - xi) are the same bits (the oracle's two directed
         //      terms, weight 1 each, sum to the same fixed-point value)
-        int head = 0, C = 0;   // ring: entries [head, head + C) mod 128
+        constexpr int RM = kEnergyRing - 1;
+        int head = 0, C = 0;   // ring: entries [head, head + C) mod kEnergyRing
         auto drain = [&](int lim) {
-            if (lane < lim) sum += energy_term(ring[(head + lane) & 127], r2min);
-            head = (head + 64) & 127;
+            if (lane < lim) sum += energy_term(ring[(head + lane) & RM], r2min);
+            head = (head + 64) & RM;
             C -= lim;
         };
         const float ox = ex_[lane], oy = ey_[lane], oz = ez_[lane];   // block 0 (own at lanes < n_own)
@@ -1476,6 +1486,30 @@ __global__ __launch_bounds__(kWave) void k_energy(DevGeom g, const float* __rest
             // partners j < S; in block 0 the lanes j > i (lanes 0..n_own-1 are all valid, so
             // clearing the lowest set bit each step drops lane i)
             unsigned long long vm = __builtin_amdgcn_ballot_w64(vj);
+#if PMC_ENERGY_STEP == 2
+            for (int i = 0; i < n_own; i += 2) {
+                const bool two = i + 1 < n_own;   // wave-uniform
+                const float xa = as_f(__builtin_amdgcn_readlane(as_i(ox), i));
+                const float ya = as_f(__builtin_amdgcn_readlane(as_i(oy), i));
+                const float za = as_f(__builtin_amdgcn_readlane(as_i(oz), i));
+                const float xb = as_f(__builtin_amdgcn_readlane(as_i(ox), i + 1));
+                const float yb = as_f(__builtin_amdgcn_readlane(as_i(oy), i + 1));
+                const float zb = as_f(__builtin_amdgcn_readlane(as_i(oz), i + 1));
+                const float r2a = pmc_r2(xa - xj, ya - yj, za - zj);
+                const float r2b = pmc_r2(xb - xj, yb - yj, zb - zj);
+                if constexpr (kFirst) vm &= vm - 1ull;
+                const unsigned long long ima = __builtin_amdgcn_ballot_w64(r2a <= rc2) & vm;
+                if constexpr (kFirst) vm &= vm - 1ull;
+                const unsigned long long imb = two ? __builtin_amdgcn_ballot_w64(r2b <= rc2) & vm : 0ull;
+                const int ca = __popcll(ima);
+                if (__builtin_amdgcn_inverse_ballot_w64(ima))
+                    ring[(head + C + mbcnt64(ima)) & RM] = as_f(as_i(r2a) | (int)sgn);
+                if (__builtin_amdgcn_inverse_ballot_w64(imb))
+                    ring[(head + C + ca + mbcnt64(imb)) & RM] = as_f(as_i(r2b) | (int)sgn);
+                C += ca + __popcll(imb);   // C < 64 + 128 <= ring size
+                while (C >= 64) drain(64);
+            }
+#else
             for (int i = 0; i < n_own; ++i) {
                 const float xi = as_f(__builtin_amdgcn_readlane(as_i(ox), i));
                 const float yi = as_f(__builtin_amdgcn_readlane(as_i(oy), i));
@@ -1484,13 +1518,16 @@ __global__ __launch_bounds__(kWave) void k_energy(DevGeom g, const float* __rest
                 if constexpr (kFirst) vm &= vm - 1ull;
                 const unsigned long long im = __builtin_amdgcn_ballot_w64(r2 <= rc2) & vm;
                 if (__builtin_amdgcn_inverse_ballot_w64(im))
-                    ring[(head + C + mbcnt64(im)) & 127] = as_f(as_i(r2) | (int)sgn);
+                    ring[(head + C + mbcnt64(im)) & RM] = as_f(as_i(r2) | (int)sgn);
                 C += __popcll(im);
                 if (C >= 64) drain(64);
             }
+#endif
         };
+#ifndef PMC_PROBE_NO_PAIRS   // analysis builds only: the per-cell cost without the pair loop
         block(0, std::true_type{});
         for (int jb = kWave; jb < S; jb += kWave) block(jb, std::false_type{});
+#endif
         if (C > 0) drain(C);
     }
     // wave sum (int64, exact in any order), one atomic per wave
@@ -1746,7 +1783,7 @@ hipError_t launch_assign(const DevGeom& g, const float* r, int64_t n_atoms, floa
 hipError_t launch_energy(const DevGeom& g, const float* disk, const int16_t* n,
                          unsigned long long* acc, hipStream_t st) {
     const int64_t total = (int64_t)g.cps_x * g.cps_y * g.nz_local;   // owned cells
-    const size_t lds = sizeof(float) * (3 * 27 * (size_t)g.nmax + 128 + 32);
+    const size_t lds = sizeof(float) * (3 * 27 * (size_t)g.nmax + kEnergyRing + 32);
     dim3 grid((unsigned)((total + kEnergyCells - 1) / kEnergyCells)), block(kWave);
     const uint32_t tc = (uint32_t)total;
     // 32-bit byte offsets below 4 GiB of disk (every single-GPU 256^3 box), else element offsets
