@@ -565,7 +565,7 @@ int pmc_stats_read(pmc_ctx* c, pmc_stats* out, int reset) {
     PMC_HIP(hipStreamSynchronize(c->stream));
     unsigned long long s[kStatCounters] = {0, 0, 0, 0};
     for (int k = 0; k < kStatCounters; ++k)
-        for (int i = 0; i < kStatSlots; ++i) s[k] += h[(size_t)k * kStatSlots + i];
+        for (int i = 0; i < kStatSlots; ++i) s[k] += h[(size_t)stat_index(k, i)];
     out->de_fixed = (int64_t)s[0];
     out->accepted = (int64_t)s[1];
     out->trials = (int64_t)s[2];
@@ -713,10 +713,10 @@ int pmc_stats_write(pmc_ctx* c, const pmc_stats* in) {
     if (!c || !in) return fail(PMC_ERR_ARG, "bad argument");
     if (int rj = slab_join(c)) return rj;
     std::vector<unsigned long long> h((size_t)kStatCounters * kStatSlots, 0ull);
-    h[0 * kStatSlots] = (unsigned long long)in->de_fixed;
-    h[1 * kStatSlots] = (unsigned long long)in->accepted;
-    h[2 * kStatSlots] = (unsigned long long)in->trials;
-    h[3 * kStatSlots] = (unsigned long long)in->evaluated;
+    h[stat_index(0, 0)] = (unsigned long long)in->de_fixed;
+    h[stat_index(1, 0)] = (unsigned long long)in->accepted;
+    h[stat_index(2, 0)] = (unsigned long long)in->trials;
+    h[stat_index(3, 0)] = (unsigned long long)in->evaluated;
     PMC_HIP(hipMemcpyAsync(c->stats, h.data(), sizeof(unsigned long long) * h.size(), hipMemcpyHostToDevice, c->stream));
     PMC_HIP(hipStreamSynchronize(c->stream));
     return PMC_OK;

@@ -26,6 +26,15 @@ __host__ __device__ constexpr int lds_floats_per_wave(int lcap) { return 3 * sub
 constexpr int kMainCap = 224;       // main launch: lds_floats_per_wave(224) * 4 B = 5120 B (32 waves/CU)
 static_assert(lds_floats_per_wave(kMainCap) * 4 <= 5120, "main-launch LDS per wave");
 constexpr int kStatCounters = 4;    // de_fixed, accepted, trials, evaluated
+// Stats layout.  PMC_STATS_LANES = 1: slot-major, the 4 counters of a slot adjacent (32 B), so a
+// cell's four counter adds are ONE wave instruction on lanes 0-3 (one 32-B memory-side atomic
+// request instead of four single-lane ones).  0: counter-major, one single-lane atomic per counter.
+#ifndef PMC_STATS_LANES
+#define PMC_STATS_LANES 1
+#endif
+__host__ __device__ constexpr int stat_index(int counter, int slot) {
+    return PMC_STATS_LANES ? slot * kStatCounters + counter : counter * kStatSlots + slot;
+}
 constexpr int kOvfHead = 2;        // ints of the subsweep overflow-queue header (pmc_kernels.hip)
 
 // Unsigned division by an invariant d: n / d = (hi + ((n - hi) >> sh1)) >> sh2, hi = umulhi(n, mul)

@@ -726,13 +726,19 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
 #ifdef PMC_PROBE_NO_STATS   // timing probe only (the counters stay zero): cost of the stats atomics
     if (lane == 0 && de_fix == 0x7fffffffffffffffll) {
 #else
-    if (lane == 0) {
+    if (PMC_STATS_LANES ? lane < kStatCounters : lane == 0) {
 #endif
         const int slot = t & (kStatSlots - 1);
-        atomicAdd(&stats[0 * kStatSlots + slot], (unsigned long long)de_fix);
-        atomicAdd(&stats[1 * kStatSlots + slot], (unsigned long long)n_acc);
-        atomicAdd(&stats[2 * kStatSlots + slot], (unsigned long long)g.n_moves);
-        atomicAdd(&stats[3 * kStatSlots + slot], (unsigned long long)n_ev);
+#if PMC_STATS_LANES
+        // lane k adds counter k: one no-return atomic instruction, 32 contiguous bytes
+        const int64_t v = lane == 0 ? de_fix : (lane == 1 ? n_acc : (lane == 2 ? g.n_moves : n_ev));
+        atomicAdd(&stats[stat_index(lane, slot)], (unsigned long long)v);
+#else
+        atomicAdd(&stats[stat_index(0, slot)], (unsigned long long)de_fix);
+        atomicAdd(&stats[stat_index(1, slot)], (unsigned long long)n_acc);
+        atomicAdd(&stats[stat_index(2, slot)], (unsigned long long)g.n_moves);
+        atomicAdd(&stats[stat_index(3, slot)], (unsigned long long)n_ev);
+#endif
     }
     PMC_STAMP(9);
     return true;
