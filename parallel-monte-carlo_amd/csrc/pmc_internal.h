@@ -17,7 +17,11 @@ constexpr int kWave = 64;          // CDNA wavefront
 #define PMC_SUBWAVES 1
 #endif
 constexpr int kSubWaves = PMC_SUBWAVES;
-constexpr int kStatSlots = 1024;   // stats accumulator slots per counter (contention spread)
+#ifndef PMC_STAT_SLOTS
+#define PMC_STAT_SLOTS 1024
+#endif
+constexpr int kStatSlots = PMC_STAT_SLOTS;   // stats accumulator slots per counter (contention spread)
+static_assert((kStatSlots & (kStatSlots - 1)) == 0, "stats slots: a power of two");
 // subsweep LDS per wave for a partner capacity lcap: x, y, z rows of `stride` slots
 // (stride = lcap rounded up to 64 with >= 32 slots of tail: the tail is the discard target of the
 // staging stores and the "far" fill past the last partner), then a term list of 2*lcap + 64.

@@ -732,7 +732,11 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
 #if PMC_STATS_LANES
         // lane k adds counter k: one no-return atomic instruction, 32 contiguous bytes
         const int64_t v = lane == 0 ? de_fix : (lane == 1 ? n_acc : (lane == 2 ? g.n_moves : n_ev));
+#ifdef PMC_PROBE_STATS_STORE   // timing probe only (wrong counters): plain stores instead of the atomics
+        stats[stat_index(lane, slot)] = (unsigned long long)v;
+#else
         atomicAdd(&stats[stat_index(lane, slot)], (unsigned long long)v);
+#endif
 #else
         atomicAdd(&stats[stat_index(0, slot)], (unsigned long long)de_fix);
         atomicAdd(&stats[stat_index(1, slot)], (unsigned long long)n_acc);
