@@ -236,12 +236,12 @@ int pmc_create(const pmc_params* params, pmc_ctx** out) {
     for (int b = 0; b < 2; ++b) {
         if ((e = hipMalloc(&c->disk[b], disk_bytes(c))) != hipSuccess) return cleanup(hip_fail(e, "hipMalloc disk"));
         if ((e = hipMalloc(&c->n[b], n_bytes(c))) != hipSuccess) return cleanup(hip_fail(e, "hipMalloc n"));
-        if ((e = hipMemset(c->disk[b], 0, disk_bytes(c))) != hipSuccess) return cleanup(hip_fail(e, "hipMemset"));
-        if ((e = hipMemset(c->n[b], 0, n_bytes(c))) != hipSuccess) return cleanup(hip_fail(e, "hipMemset"));
+        if ((e = hipMemsetAsync(c->disk[b], 0, disk_bytes(c), c->stream)) != hipSuccess) return cleanup(hip_fail(e, "hipMemset"));
+        if ((e = hipMemsetAsync(c->n[b], 0, n_bytes(c), c->stream)) != hipSuccess) return cleanup(hip_fail(e, "hipMemset"));
     }
     const size_t sb = sizeof(unsigned long long) * kStatCounters * kStatSlots;
     if ((e = hipMalloc(&c->stats, sb)) != hipSuccess) return cleanup(hip_fail(e, "hipMalloc stats"));
-    if ((e = hipMemset(c->stats, 0, sb)) != hipSuccess) return cleanup(hip_fail(e, "hipMemset"));
+    if ((e = hipMemsetAsync(c->stats, 0, sb, c->stream)) != hipSuccess) return cleanup(hip_fail(e, "hipMemset"));
     if ((e = hipMalloc(&c->eacc, sizeof(unsigned long long) * kStatSlots)) != hipSuccess)
         return cleanup(hip_fail(e, "hipMalloc eacc"));
     if ((e = hipMalloc(&c->flags, 16)) != hipSuccess) return cleanup(hip_fail(e, "hipMalloc flags"));
@@ -250,10 +250,17 @@ int pmc_create(const pmc_params* params, pmc_ctx** out) {
         // header (queue length, done counter: zero between launches) + one entry per cell
         const size_t ob = sizeof(int) * (kOvfHead + per_colour);
         if ((e = hipMalloc(&c->ovf, ob)) != hipSuccess) return cleanup(hip_fail(e, "hipMalloc ovf"));
-        if ((e = hipMemset(c->ovf, 0, ob)) != hipSuccess) return cleanup(hip_fail(e, "hipMemset"));
+        if ((e = hipMemsetAsync(c->ovf, 0, ob, c->stream)) != hipSuccess) return cleanup(hip_fail(e, "hipMemset"));
         c->ovf_bytes = ob;
     }
-    if ((e = hipMemset(c->flags, 0, 16)) != hipSuccess) return cleanup(hip_fail(e, "hipMemset"));
+    if ((e = hipMemsetAsync(c->flags, 0, 16, c->stream)) != hipSuccess) return cleanup(hip_fail(e, "hipMemset"));
+    // Every zeroing above runs on the context stream and is complete before the context is
+    // returned.  (It used to be hipMemset on the null stream, which a hipStreamNonBlocking stream
+    // does not wait for and which may still be queued when hipMemset returns: with the null stream
+    // busy -- torch's default stream, RCCL set-up work -- the zeroing of n could land after
+    // init_lattice's assign had written the counts on the context stream, and a fresh context read
+    // back all-zero counts.  tests/test_gpu_parity.py::test_create_ordered_after_busy_null_stream.)
+    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return cleanup(hip_fail(e, "hipStreamSynchronize"));
     if ((e = hipEventCreate(&c->ev0)) != hipSuccess) return cleanup(hip_fail(e, "hipEventCreate"));
     if ((e = hipEventCreate(&c->ev1)) != hipSuccess) return cleanup(hip_fail(e, "hipEventCreate"));
     *out = c;
@@ -454,7 +461,8 @@ int pmc_phase_range_on(pmc_ctx* c, int colour, uint32_t sweep, int zl_begin, int
     if (st == c->stream) return pmc_phase_range(c, colour, sweep, zl_begin, zl_end);
     if (!c->ovf_aux) {   // the aux launches' own overflow queue (concurrent with the context stream's)
         PMC_HIP(hipMalloc(&c->ovf_aux, c->ovf_bytes));
-        PMC_HIP(hipMemset(c->ovf_aux, 0, c->ovf_bytes));
+        PMC_HIP(hipMemsetAsync(c->ovf_aux, 0, c->ovf_bytes, c->stream));   // ordered before st's launches:
+        PMC_HIP(hipStreamSynchronize(c->stream));                         // st does not wait for c->stream
     }
     int o[3];
     pmc_colour_offset(colour, o);
@@ -1190,10 +1198,16 @@ int slab_attach(pmc_ctx* c, int rank, int world, bool messages) {
         }
     // overflow queues of the upper and the boundary chain (they run beside the context stream's)
     for (int** q : {&c->ovf_aux, &c->ovf_b})
-        if (!*q && ((e = hipMalloc(q, c->ovf_bytes)) != hipSuccess || (e = hipMemset(*q, 0, c->ovf_bytes)) != hipSuccess)) {
+        if (!*q && ((e = hipMalloc(q, c->ovf_bytes)) != hipSuccess ||
+                    (e = hipMemsetAsync(*q, 0, c->ovf_bytes, c->stream)) != hipSuccess)) {
             drop_slab(c);
             return hip_fail(e, "hipMalloc overflow queue");
         }
+    // the queues' zeroing and the initial event records complete before any stream uses them
+    if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) {
+        drop_slab(c);
+        return hip_fail(e, "hipStreamSynchronize");
+    }
     (void)messages;   // halo messages go straight from and into the state buffers
     return PMC_OK;
 }
@@ -1214,30 +1228,6 @@ int pmc_slab_init(pmc_ctx* c, int rank, int world, const unsigned char* id) {
     if (r != ncclSuccess) {
         s->comm = nullptr;
         rc = nccl_fail(r, "ncclCommInitRank");
-        drop_slab(c);
-        return rc;
-    }
-    // Warm-up: one small message each way with both neighbours (the peers every exchange uses), then
-    // the whole device.  RCCL sets up peer connections lazily, with device allocations and work of
-    // its own; finishing that here keeps it from overlapping this process's later allocations and
-    // launches (a whole-box context created right after a one-rank RCCL slab has read back zero
-    // counts on a fresh box, intermittently).  Collective, like the communicator creation.
-    void* tmp = nullptr;
-    hipError_t e = hipMalloc(&tmp, 64);
-    if (e == hipSuccess) e = hipMemset(tmp, 0, 64);
-    if (e != hipSuccess) {
-        if (tmp) (void)hipFree(tmp);
-        drop_slab(c);
-        return hip_fail(e, "slab warm-up buffer");
-    }
-    xfer_send(s, (char*)tmp, 8, s->below);
-    xfer_send(s, (char*)tmp + 8, 8, s->above);
-    xfer_recv(s, (char*)tmp + 32, 8, s->above);
-    xfer_recv(s, (char*)tmp + 40, 8, s->below);
-    rc = xfer_run(s);
-    if (rc == PMC_OK && (e = hipDeviceSynchronize()) != hipSuccess) rc = hip_fail(e, "slab warm-up");
-    (void)hipFree(tmp);
-    if (rc) {
         drop_slab(c);
         return rc;
     }
@@ -1443,12 +1433,13 @@ int pmc_slab_observables(pmc_ctx* c, int with_energy, pmc_stats* out, double* e_
         if (!R.all_reduce) return fail(PMC_ERR_HIP, "librccl lacks ncclAllReduce");
         void* d = nullptr;
         PMC_HIP(hipMalloc(&d, sizeof v));
-        hipError_t e = hipMemcpy(d, v, sizeof v, hipMemcpyHostToDevice);
+        // every copy on aux, the stream the all-reduce runs on (no null-stream work in between)
+        hipError_t e = hipMemcpyAsync(d, v, sizeof v, hipMemcpyHostToDevice, s->aux);
         if (e != hipSuccess) { (void)hipFree(d); return hip_fail(e, "observables copy"); }
         ncclResult_t r = R.all_reduce(d, d, 5, ncclUint64, ncclSum, s->comm, s->aux);
         if (r != ncclSuccess) { (void)hipFree(d); return nccl_fail(r, "ncclAllReduce"); }
-        e = hipStreamSynchronize(s->aux);
-        if (e == hipSuccess) e = hipMemcpy(v, d, sizeof v, hipMemcpyDeviceToHost);
+        e = hipMemcpyAsync(v, d, sizeof v, hipMemcpyDeviceToHost, s->aux);
+        if (e == hipSuccess) e = hipStreamSynchronize(s->aux);
         (void)hipFree(d);
         if (e != hipSuccess) return hip_fail(e, "observables all-reduce");
     } else if (s->group) {

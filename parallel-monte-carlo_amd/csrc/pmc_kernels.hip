@@ -977,11 +977,11 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_fallback(DevGeom
     // the queue is cleared for the next launch (no memset between launches; graph replays start
     // from a clean queue): a one-workgroup grid clears it itself; otherwise the last workgroup to
     // finish (every workgroup has read the count by then) does
+    __syncthreads();   // every wave of the workgroup has read the count
     if (gridDim.x == 1) {
         if (threadIdx.x == 0 && count != 0) ovf[kOvfCount] = 0;
         return;
     }
-    __syncthreads();
     if (threadIdx.x == 0) {
         __threadfence();
         if (atomicAdd(&ovf[kOvfDone], 1) == (int)gridDim.x - 1) {

@@ -406,10 +406,14 @@ class SlabDriver:
 
     def __init__(self, cps: int, nz_local: int, rank: int, world: int, stream=None, atoms_per_rank: int = 0,
                  atoms_total: int = 0, nmax: int = 16, n_moves: int = 10, seed: int = 1234,
-                 use_rccl: Optional[bool] = None, group=None, local_group=None, cps_y: int = 0):
+                 use_rccl: Optional[bool] = None, group=None, local_group=None, cps_y: int = 0,
+                 flags: int = 0, lattice_cps_z: int = 0):
         """local_group: a pmc_amd.engine.LocalGroup -- the in-process transport (this rank is one of
         local_group.world slab contexts of this process; construct and drive each rank from its
-        own thread: the exchanges are collective)."""
+        own thread: the exchanges are collective).  flags: pmc_params.flags (PMC_FLAG_FULL_SHUFFLE:
+        the reference-like colour order, up to 8 runs and exchanges per sweep).  lattice_cps_z with
+        atoms_total: the lattice of atoms_total particles over a box lattice_cps_z cells tall
+        (pmc_init_lattice_planes; the config-5 weak-scaling start), else over this box."""
         from .engine import PmcContext, comm_unique_id
         self.g = SlabGeometry(cps, nz_local, rank, world, nmax)
         if stream is None and local_group is None:
@@ -417,7 +421,7 @@ class SlabDriver:
             stream = torch.cuda.Stream()
         self.stream = stream
         self.ctx = PmcContext(cps, cps_y=cps_y, cps_z=self.g.cps_z, nz_local=nz_local, z0=self.g.z0, halo=1,
-                              nmax=nmax, n_moves=n_moves, seed=seed,
+                              nmax=nmax, n_moves=n_moves, seed=seed, flags=flags,
                               stream=stream.cuda_stream if stream is not None else None)
         self.cps_y = cps_y or cps
         if local_group is not None:
@@ -442,7 +446,10 @@ class SlabDriver:
                     buf = on.cpu()
                 uid = bytes(buf.numpy().tobytes())
             self.ctx.slab_init(rank, world, uid)      # RCCL communicator: collective over the ranks
-        if atoms_total:
+        if atoms_total and lattice_cps_z:
+            self.ctx.init_lattice_planes(atoms_total, lattice_cps_z)
+            self.ctx.slab_exchange()
+        elif atoms_total:
             self.ctx.init_lattice_global(atoms_total)
             self.ctx.slab_exchange()
         elif atoms_per_rank:

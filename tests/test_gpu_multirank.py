@@ -50,27 +50,37 @@ def _window(oracle, count):
     raise AssertionError("no window")
 
 
-@pytest.mark.parametrize("world,cps,cps_y,cps_z,atoms", [
-    (2, 16, 16, 16, 10_000),
-    (3, 16, 16, 12, 7_500),
-    (4, 16, 16, 16, 10_000),
-    (8, 16, 16, 16, 10_000),      # 2 planes per rank: no interior launch at all
-    (4, 32, 32, 32, 120_000),
-    (2, 12, 20, 16, 9_000),      # rectangular x/y
+FULL = 1   # PMC_FLAG_FULL_SHUFFLE: the reference-like colour order (up to 8 runs, 8 exchanges a sweep)
+
+
+@pytest.mark.parametrize("world,cps,cps_y,cps_z,atoms,flags", [
+    (2, 16, 16, 16, 10_000, 0),
+    (3, 16, 16, 12, 7_500, 0),
+    (4, 16, 16, 16, 10_000, 0),
+    (8, 16, 16, 16, 10_000, 0),      # 2 planes per rank: no interior launch at all
+    (4, 32, 32, 32, 120_000, 0),
+    (2, 12, 20, 16, 9_000, 0),       # rectangular x/y
+    (2, 16, 16, 16, 10_000, FULL),
+    (4, 16, 16, 16, 10_000, FULL),
+    (4, 32, 32, 32, 120_000, FULL),
 ])
-def test_c_slab_driver_world_equals_oracle(pmc, oracle, world, cps, cps_y, cps_z, atoms):
+def test_c_slab_driver_world_equals_oracle(pmc, oracle, world, cps, cps_y, cps_z, atoms, flags):
     from pmc_amd.engine import LocalGroup
     from pmc_amd.slab import SlabDriver
     nz = cps_z // world
     count = 8
     first = _window(oracle, count)
+    if flags:   # the window has runs of one colour parity shorter than 4 (more exchanges)
+        runs = [sum(1 for k in range(1, 8) if o[k] % 2 != o[k - 1] % 2) + 1
+                for o, _, _ in (oracle.sweep_plan(1234, first + j, 2.5, flags) for j in range(count))]
+        assert max(runs) > 2, runs
     pmc.lib()
     group = LocalGroup(world)
     drivers = [None] * world
 
     def rank_main(r):
         d = SlabDriver(cps=cps, cps_y=cps_y, nz_local=nz, rank=r, world=world, atoms_total=atoms,
-                       local_group=group)
+                       local_group=group, flags=flags)
         drivers[r] = d
         d.run(first, count)
         d.ctx.synchronize()
@@ -78,7 +88,7 @@ def test_c_slab_driver_world_equals_oracle(pmc, oracle, world, cps, cps_y, cps_z
         return d.owned(), d.ctx.stats(), d.ctx.energy(), d.ctx.error_flags(), obs
 
     res = _run_ranks(world, rank_main)
-    st = oracle.OracleState(oracle.make_params(cps=cps, cps_y=cps_y, cps_z=cps_z))
+    st = oracle.OracleState(oracle.make_params(cps=cps, cps_y=cps_y, cps_z=cps_z, flags=flags))
     assert st.init_lattice(atoms) == 0
     assert st.run(first, count) == 0
     plane, row = cps * cps_y, 3 * 16
@@ -219,3 +229,73 @@ print("ok")
                          env=dict(os.environ, PMC_SLAB_CHAINS="1"), capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-3000:]
     assert "ok" in out.stdout
+
+
+def _world_vs_oracle(pmc, oracle, world, cps, nz, atoms, first, count, lattice_cps_z=0, threads=16):
+    """World ranks of the C slab driver (in-process transport, one GPU) over `count` sweeps of the
+    cps x cps x world*nz box against the oracle's whole-box run: every occupied slot, counts, the
+    four counters (summed over ranks and through pmc_slab_observables) and the energy."""
+    from pmc_amd.engine import LocalGroup
+    from pmc_amd.slab import SlabDriver
+    pmc.lib()
+    group = LocalGroup(world)
+    drivers = [None] * world
+
+    def rank_main(r):
+        d = SlabDriver(cps=cps, nz_local=nz, rank=r, world=world, atoms_total=atoms, local_group=group,
+                       lattice_cps_z=lattice_cps_z)
+        drivers[r] = d
+        d.run(first, count)
+        d.ctx.synchronize()
+        obs = d.ctx.slab_observables()
+        return d.owned(), d.ctx.stats(), d.ctx.error_flags(), obs
+
+    res = _run_ranks(world, rank_main, timeout=600)
+    for d in drivers:      # device memory back before the oracle's host arrays grow
+        d.ctx.close()
+    group.close()
+    oracle.set_threads(threads)
+    st = oracle.OracleState(oracle.make_params(cps=cps, cps_z=world * nz))
+    assert st.init_lattice(atoms) == 0
+    assert int(st.n.sum()) == atoms
+    assert st.run(first, count) == 0
+    plane, row = cps * cps, 3 * 16
+    tot = {"de_fixed": 0, "accepted": 0, "trials": 0, "evaluated": 0}
+    for r, ((d, n), s, fl, _) in enumerate(res):
+        ref = slice(r * nz * plane, (r + 1) * nz * plane)
+        assert np.array_equal(n, st.n[ref]), f"rank {r}: counts differ"
+        assert oracle.valid_slots_equal(d, n, st.disk[ref.start * row:ref.stop * row], st.n[ref], 16), \
+            f"rank {r}: coordinates differ"
+        assert fl == 0
+        for k in tot:
+            tot[k] += s[k]
+    o = st.stats.as_dict()
+    assert tot == o
+    assert o["trials"] == count * 10 * atoms
+    e = st.energy()
+    for *_, (obs, e_all) in res:
+        assert obs == o
+        assert e_all == e
+    return o
+
+
+@pytest.mark.timeout(400)
+def test_config4_world8_128_equals_oracle(pmc, oracle):
+    """BASELINE config 4 at its workload: the 128^3-cell, 1e7-particle box in 8 z-slabs of 16
+    planes (pmc_init_lattice_global: every rank starts from its planes of the one-GPU lattice),
+    three sweeps of the product slab driver -- sweeps 13-15 shift along z in both directions --
+    against the oracle's whole-box run bit for bit (start.cu:237-260 is the loop partitioned)."""
+    plans = [oracle.sweep_plan(1234, s, 2.5) for s in (13, 14, 15)]
+    assert {(f, d > 0) for _, f, d in plans} >= {(2, True), (2, False)}
+    _world_vs_oracle(pmc, oracle, world=8, cps=128, nz=16, atoms=10_000_000, first=13, count=3)
+
+
+@pytest.mark.timeout(600)
+def test_config5_world8_256_equals_oracle(pmc, oracle):
+    """BASELINE config 5 at its workload: 8 slabs of 256x256x32 cells, together the 256^3-cell box
+    with the 8e7-particle lattice (each rank keeps its planes of it, pmc_init_lattice_planes), two
+    sweeps with z shifts both ways, against the oracle's whole 256^3 box bit for bit."""
+    plans = [oracle.sweep_plan(1234, s, 2.5) for s in (13, 14)]
+    assert {(f, d > 0) for _, f, d in plans} == {(2, True), (2, False)}
+    _world_vs_oracle(pmc, oracle, world=8, cps=256, nz=32, atoms=80_000_000, first=13, count=2,
+                     lattice_cps_z=256)

@@ -47,6 +47,26 @@ def test_detmath_device_equals_host(pmc, oracle):
         assert oracle.lib().orc_to_fixed(float(out_f[i, 3])) == int(out_d[i, 1])
 
 
+def test_create_ordered_after_busy_null_stream(pmc):
+    """pmc_create's zeroing is ordered before the context's own work.  A spin kernel keeps the null
+    stream (torch's default stream) busy; a context created meanwhile must still bin the lattice,
+    because its zeroing runs on its own (non-blocking) stream and completes inside pmc_create.  The
+    round-2 library zeroed with hipMemset on the null stream, which the context stream does not
+    wait for: the zeroing of n then landed after init_lattice's counts (the intermittent all-zero
+    count readback of test_gpu_c_slab_driver_equals_whole_box)."""
+    import torch
+    assert torch.cuda.current_stream().cuda_stream == 0, "torch's current stream is not the null stream"
+    torch.cuda._sleep(200_000_000)          # ~0.1-2 s of spinning on the null stream
+    ctx = pmc.PmcContext(16)
+    ctx.init_lattice(10_000)
+    disk, n = ctx.copy_out()                 # on the context stream: the spin may still be running
+    busy = not torch.cuda.default_stream().query()
+    torch.cuda.synchronize()
+    assert int(n.sum()) == 10_000, f"counts read back wrong while the null stream was busy={busy}"
+    n2 = ctx.copy_out()[1]
+    assert np.array_equal(n, n2), "counts changed after the null stream drained"
+
+
 @pytest.mark.parametrize("cps,atoms", [(16, 10_000), (64, 1_000_000)])
 def test_lattice_assign_parity(pmc, oracle, cps, atoms):
     ctx = _ctx(pmc, cps)
