@@ -123,7 +123,7 @@ def host_cpu() -> dict:
             "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
 
 
-def cpu_baseline(disk, n, cps: int, sweep0: int, serial_planes: int) -> tuple[dict, object]:
+def cpu_baseline(disk, n, cps: int, sweep0: int, serial_planes: int, cps_z: int = 0) -> tuple[dict, object]:
     """The C oracle (the reference has no CPU path: SURVEY.md 0/8c) timed on this host:
     (i) serial, one core: one colour phase over planes [0, serial_planes);
     (ii) OpenMP over the cells of a colour on the cores of one socket (one thread per physical
@@ -133,8 +133,11 @@ def cpu_baseline(disk, n, cps: int, sweep0: int, serial_planes: int) -> tuple[di
     import pmc_oracle  # test infrastructure: timed CPU baseline only
     pmc_oracle.build()
     host = host_cpu()
+    cps_z = cps_z or cps
+    box = f"{cps}^3" if cps_z == cps else f"{cps}x{cps}x{cps_z}"
+    serial_planes = min(serial_planes, cps_z)
     # (i) serial
-    st1 = pmc_oracle.OracleState(pmc_oracle.make_params(cps=cps))
+    st1 = pmc_oracle.OracleState(pmc_oracle.make_params(cps=cps, cps_z=cps_z))
     st1.disk[:] = disk
     st1.n[:] = n
     pmc_oracle.set_threads(1)
@@ -151,7 +154,7 @@ def cpu_baseline(disk, n, cps: int, sweep0: int, serial_planes: int) -> tuple[di
     if host["cgroup_cpu_quota"] and host["cgroup_cpu_quota"] < threads:
         threads = max(1, int(host["cgroup_cpu_quota"]))
         limited_by = "cgroup CPU quota"
-    st = pmc_oracle.OracleState(pmc_oracle.make_params(cps=cps))
+    st = pmc_oracle.OracleState(pmc_oracle.make_params(cps=cps, cps_z=cps_z))
     st.disk[:] = disk
     st.n[:] = n
     used = pmc_oracle.set_threads(threads)
@@ -161,11 +164,11 @@ def cpu_baseline(disk, n, cps: int, sweep0: int, serial_planes: int) -> tuple[di
     par = st.stats.trials / dt
     cores_socket = host["cores_per_socket"] or threads
     out = {"value": par, "unit": "trial-moves/s", "cores": threads, "kind": "port",
-           "sample": f"one full sweep of the {cps}^3 box from the GPU state, C oracle, OpenMP over the cells "
+           "sample": f"one full sweep of the {box} box from the GPU state, C oracle, OpenMP over the cells "
                      f"of a colour on {threads} threads (one per physical core of socket 0; limited by "
                      f"{limited_by}), {dt:.2f} s",
            "serial": {"value": serial, "cores": 1,
-                      "sample": f"one colour phase over planes [0,{serial_planes}) of the {cps}^3 box, 1 thread, "
+                      "sample": f"one colour phase over planes [0,{serial_planes}) of the {box} box, 1 thread, "
                                 f"{dt1:.2f} s"},
            "parallel_efficiency": par / (serial * threads),
            "socket_cores": cores_socket,
@@ -204,15 +207,80 @@ def parity_leg(sim, one_sweep, disk0, n0, sweep0: int, sweeps: int, e0: float, o
             "counters_equal": g == c, "state_bitwise_equal": same}
 
 
-def traffic_from_profile() -> dict | None:
+def parity_leg_slab(ctx, one_sweep, finish, disk_s, n_s, sweep0: int, e0: float, gather, ost, rank: int) -> dict | None:
+    """parity_leg for the slab driver, collective over the ranks: every rank restores its storage
+    (owned planes and halos) at the timed start, reruns the CPU sample's sweep, the whole box's
+    counters and energy come from pmc_slab_observables (fixed-point sums over the ranks), the owned
+    planes are gathered on rank 0 and compared with the oracle's whole-box result there."""
+    ctx.copy_in(disk_s, n_s)
+    ctx.slab_exchange()
+    ctx.stats(reset=True)
+    one_sweep(sweep0)
+    finish()
+    ctx.synchronize()
+    g, e_gpu = ctx.slab_observables(True)
+    d, n = ctx.copy_out()
+    whole = gather(d, n)
+    if rank != 0:
+        return None
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pmc_oracle  # test infrastructure: the checker, never the measured path
+    disk_g, n_g = whole
+    c = ost.stats.as_dict()
+    e_cpu = ost.energy()
+    same = bool(np.array_equal(n_g, ost.n)) and pmc_oracle.valid_slots_equal(disk_g, n_g, ost.disk, ost.n, ost.nmax)
+    acc_g = g["accepted"] / g["trials"] if g["trials"] else 0.0
+    acc_c = c["accepted"] / c["trials"] if c["trials"] else 0.0
+    rel = lambda a, b: abs(a - b) / abs(b) if b else abs(a - b)  # noqa: E731
+    return {"reference": "C oracle (corrected-mode restatement of subsweep.h / shiftCells.h), whole box",
+            "sweeps": 1, "first_sweep": sweep0, "energy_start": e0,
+            "energy_gpu": e_gpu, "energy_cpu": e_cpu, "energy_rel_err": rel(e_gpu, e_cpu),
+            "acceptance_gpu": acc_g, "acceptance_cpu": acc_c, "acceptance_rel_err": rel(acc_g, acc_c),
+            "counters_equal": g == c, "state_bitwise_equal": same,
+            "gpu_side": "all ranks (slab driver), owned planes gathered on rank 0"}
+
+
+def make_gather(world: int, rank: int, plane: int, nz: int, row: int):
+    """gather(disk_storage, n_storage) -> (disk, n) of the whole box on rank 0 (None elsewhere): the
+    owned planes of every rank in rank order (rank r owns global planes [r*nz, (r+1)*nz)).
+    Collective; counts travel as bytes (RCCL has no 16-bit integer type)."""
+    def gather(disk_s, n_s):
+        own_d = np.ascontiguousarray(disk_s[plane * row:(nz + 1) * plane * row])
+        own_n = np.ascontiguousarray(n_s[plane:(nz + 1) * plane])
+        if world == 1:
+            return own_d, own_n
+        import torch
+        import torch.distributed as dist
+        dev = "cuda" if dist.get_backend() == "nccl" else "cpu"     # (gloo: the CPU tests)
+        td = torch.from_numpy(own_d).to(dev)
+        tn = torch.from_numpy(own_n.view(np.uint8)).to(dev)
+        ld = [torch.empty_like(td) for _ in range(world)] if rank == 0 else None
+        ln = [torch.empty_like(tn) for _ in range(world)] if rank == 0 else None
+        dist.gather(td, ld, dst=0)
+        dist.gather(tn, ln, dst=0)
+        if rank != 0:
+            return None
+        disk = np.concatenate([t.cpu().numpy() for t in ld])
+        n = np.concatenate([t.cpu().numpy() for t in ln]).view(np.int16)
+        return disk, n
+    return gather
+
+
+def traffic_from_profile(config: str, slab: bool, nz_local: int) -> dict | None:
+    """Measured memory-side traffic per dominant-kernel launch (profiles/pmc_traffic.json, from
+    rocprofv3 FETCH_SIZE / WRITE_SIZE passes): the whole box at top level, slab launch shapes under
+    "slab" keyed "<config>:<planes per rank>" (tools/slab_traffic.sh)."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return None
     try:
         with open(path) as f:
-            return json.load(f)
+            t = json.load(f)
     except Exception:
         return None
+    if not slab:
+        return t
+    return (t.get("slab") or {}).get(f"{config}:{nz_local}")
 
 
 
@@ -279,6 +347,9 @@ def main() -> int:
     ap.add_argument("--self-rccl", action="store_true",
                     help="one slab rank: halos through a one-rank RCCL communicator (default for config 5)")
     ap.add_argument("--local-halo", action="store_true", help="config 5 at N=1: local halo copies, no RCCL")
+    ap.add_argument("--emulate-ranks", type=int, default=0,
+                    help="config 4 at N=1: one rank's slab of an R-rank run (the bottom 128/R planes of the "
+                         "1e7 lattice as a periodic slab) -- the per-rank launch shapes, for rocprof")
     args = ap.parse_args()
 
     import torch
@@ -291,6 +362,10 @@ def main() -> int:
     if world != args.gpus and world > 1:
         print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}", file=sys.stderr)
     config = args.config or ("4" if args.strong else ("3" if world == 1 else "4"))
+    if args.emulate_ranks:
+        if config != "4" or world != 1:
+            raise SystemExit("--emulate-ranks is a one-process rehearsal of config 4")
+        args.slab = True
     if config == "4" and world == 1 and not args.slab:
         config = "3"          # the 1-GPU point of the config-4 strong-scaling curve is config 3
     if config == "5box" and world > 1:
@@ -311,7 +386,10 @@ def main() -> int:
     else:
         cps, atoms = 256, 80_000_000
     slab = config in ("4", "5") or args.slab
-    if config == "4" or (config == "3" and slab):
+    if args.emulate_ranks:
+        nz_local = cps // args.emulate_ranks
+        box_z = nz_local
+    elif config == "4" or (config == "3" and slab):
         nz_local = cps // world
         box_z = cps
     elif config == "5":
@@ -343,8 +421,8 @@ def main() -> int:
         from pmc_amd.slab import SlabDriver
         use_rccl = world > 1 or args.self_rccl or (config == "5" and not args.local_halo)
         drv = SlabDriver(cps=cps, nz_local=nz_local, rank=rank, world=world, stream=stream, use_rccl=use_rccl)
-        if config == "5":
-            drv.ctx.init_lattice_planes(atoms, cps)     # this rank's planes of the 256^3 / 8e7 lattice
+        if config == "5" or args.emulate_ranks:
+            drv.ctx.init_lattice_planes(atoms, cps)     # this rank's planes of the 256^3 / 8e7 (128^3 / 1e7) lattice
         else:
             drv.ctx.init_lattice_global(atoms)         # this rank's planes of the one 128^3 box
         drv.ctx.slab_exchange()
@@ -374,10 +452,19 @@ def main() -> int:
     else:
         n_owned = n_h[plane:plane * (nz_local + 1)].astype(np.int64)
         stencil = slab_stencil_counts(n_h, cps, nz_local)
-        # the context-stream launches are the interior planes [1, nz-1): each cell once per sweep
-        inner = slice(plane, plane * (nz_local - 1))
-        sub_launch_bytes = staged_bytes(n_owned[inner], stencil[inner]) / 8.0
-        roof_kernel = "k_subsweep<16,16,true> (interior planes of a slab colour phase)"
+        # kind-0 launches: the two interior chains, planes [1, zs) and [zs, nz-1) (pmc_slab_sweep;
+        # one chain when zs < 2 or PMC_SLAB_CHAINS=1), one launch per chain and colour phase; the
+        # roofline's bytes per launch are their mean (the chains run concurrently)
+        zs = 2 * (nz_local // 4)
+        if zs < 2 or os.environ.get("PMC_SLAB_CHAINS") == "1":
+            zs = nz_local - 1
+        chains = [(1, zs)] + ([(zs, nz_local - 1)] if nz_local - 1 > zs else [])
+        chains = [(a, b) for a, b in chains if b > a]
+        per_chain = [staged_bytes(n_owned[a * plane:b * plane], stencil[a * plane:b * plane]) / 8.0
+                     for a, b in chains]
+        sub_launch_bytes = sum(per_chain) / len(per_chain) if per_chain else 0.0
+        roof_kernel = ("k_subsweep<16,16,true> (a slab colour phase's interior launches, planes "
+                       + " and ".join(f"[{a},{b})" for a, b in chains) + ", mean bytes per launch)")
     e_start = sim.energy()      # cell-list energy of the state the timed region starts from
     # The host analysis above leaves the GPU idle, and an idle MI355X comes back at a lower clock:
     # after a 0.5 s gap the first sweeps take 3.0-3.3 ms and the rate settles at 2.53 ms only
@@ -415,11 +502,11 @@ def main() -> int:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        tr = torch.tensor([trials_local], dtype=torch.int64, device="cuda")
+        tr = torch.tensor([trials_local, st["accepted"]], dtype=torch.int64, device="cuda")
         dist.all_reduce(tr)
-        trials_total = int(tr.item())
+        trials_total, accepted_total = (int(v) for v in tr.tolist())
     else:
-        trials_total = trials_local
+        trials_total, accepted_total = trials_local, st["accepted"]
     flags = sim.error_flags()
     value = trials_total / elapsed
     # energy bookkeeping over the timed sweeps: E_start + sum of accepted dE (fixed point 2^-32,
@@ -440,27 +527,56 @@ def main() -> int:
         n_launch = tm["n_subsweep"]
         avg_launch_s = (tm["subsweep_ms"] / n_launch * 1e-3) if n_launch else None
         achieved = (sub_launch_bytes / avg_launch_s / 1e9) if avg_launch_s else None
-        traffic = traffic_from_profile()
+        traffic = traffic_from_profile(config, slab, nz_local)
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                "traffic": traffic.get("subsweep_bytes_per_launch") if (traffic and not slab) else None,
+                "traffic": traffic.get("subsweep_bytes_per_launch") if traffic else None,
+                "traffic_source": traffic.get("source") if traffic else None,
                 "kernel": roof_kernel,
                 "launch_ms": avg_launch_s * 1e3 if avg_launch_s else None,
                 "launches_timed": n_launch,
                 "shift_ms": tm["shift_ms"] / tm["n_shift"] if tm["n_shift"] else None,
                 "boundary_launch_ms": tm["boundary_ms"] / tm["n_boundary"] if tm["n_boundary"] else None,
                 "algorithmic_bytes_per_launch": sub_launch_bytes}
-        cpu = None
-        parity = None
-        if not args.no_cpu_baseline and not slab:
-            try:
-                sp = args.serial_planes or min(cps, 128)
-                cpu, ost = cpu_baseline(disk_h, n_h, cps, first, sp)
-                parity = parity_leg(sim, one_sweep, disk_h, n_h, first, 1, e_start, ost)
-            except Exception as e:  # the baseline is reported, never the measured value
-                cpu = {"error": repr(e)}
+    # CPU baseline and parity leg (after the timed region).  Slabs: the start state of the timed
+    # region is gathered on rank 0 (the whole box), the oracle runs there while the other ranks wait,
+    # then every rank reruns the sample's sweep (collective) and rank 0 compares.
+    cpu = None
+    parity = None
+    if not args.no_cpu_baseline:
+        sp = args.serial_planes or min(cps, 128)
+        ost = None
+        if not slab:
+            if rank == 0:
+                try:
+                    cpu, ost = cpu_baseline(disk_h, n_h, cps, first, sp)
+                    parity = parity_leg(sim, one_sweep, disk_h, n_h, first, 1, e_start, ost)
+                except Exception as e:  # the baseline is reported, never the measured value
+                    cpu = {"error": repr(e)}
+        else:
+            gather = make_gather(world, rank, plane, nz_local, 3 * 16)
+            whole = gather(disk_h, n_h)
+            if rank == 0:
+                try:
+                    cpu, ost = cpu_baseline(whole[0], whole[1], cps, first, sp, cps_z=box_z)
+                    cpu["sample"] += f" (whole {cps}x{cps}x{box_z} box gathered from {world} rank(s))"
+                except Exception as e:
+                    cpu = {"error": repr(e)}
+            del whole
+            barrier()
+            ok = torch.tensor([1 if (rank != 0 or ost is not None) else 0], device="cuda")
+            if world > 1:
+                dist.broadcast(ok, src=0)
+            if int(ok.item()):
+                parity = parity_leg_slab(sim, one_sweep, finish, disk_h, n_h, first, e_start, gather, ost, rank)
+
+    if rank == 0:
         sweeps_per_s = args.steps / elapsed
         name = CONFIG_NAMES[config].format(n=world, nz=nz_local, cz=box_z)
+        if args.emulate_ranks:
+            name = (f"rehearsal of BASELINE config 4 at {args.emulate_ranks} ranks on 1 MI355X: one rank's slab "
+                    f"({nz_local} planes of the 128^3 / 1e7 box, periodic, halos through "
+                    + ("RCCL" if use_rccl else "local copies") + "); value = ONE rank's rate")
         out = {
             "metric": "MC trial-moves/s (whole node)",
             "value": value,
@@ -470,8 +586,12 @@ def main() -> int:
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "strong" if config == "4" else "weak",
-            "vs_baseline": None,
+            # configs 3 -> 4 are one fixed box over 1..N GPUs (strong); config 5 fixes the work per GPU
+            "scaling": "weak" if config == "5" else "strong",
+            # the same run's CPU baseline (one socket of the host, C oracle): BASELINE.json publishes
+            # no number, so the socket estimate is the denominator
+            "vs_baseline": (value / cpu["socket_estimate"]) if (cpu and cpu.get("socket_estimate")) else None,
+            "vs_baseline_of": "cpu_baseline.socket_estimate" if (cpu and cpu.get("socket_estimate")) else None,
             "dtype": "f32",
             "data": "synthetic (reference simple-cubic lattice start, Philox seed 1234)",
             "config": {"workload": name, "baseline_config": config,
@@ -479,7 +599,7 @@ def main() -> int:
                        "particles": particles, "n_moves": 10, "nmax": 16, "beta": 0.3, "sigma": 0.5,
                        "w": 2.5, "parallelism": transport},
             "sweeps_per_s": sweeps_per_s,
-            "acceptance": st["accepted"] / st["trials"] if st["trials"] else None,
+            "acceptance": accepted_total / trials_total if trials_total else None,
             "energy": {"start": e_start, "end": e_end, "start_plus_sum_dE": e_start + de_timed,
                        "per_particle_end": e_end / particles if particles else None,
                        "bookkeeping_rel_err": abs(e_start + de_timed - e_end) / abs(e_end) if e_end else None,

@@ -165,9 +165,12 @@ int pmc_phase_range_on(pmc_ctx* ctx, int colour, uint32_t sweep, int zl_begin, i
  * Replaces the reference's single-GPU main loop (start.cu:237-260) for a box split into z-slabs:
  * rank r owns planes [r*nz_local, (r+1)*nz_local) of a cps_x x cps_y x (world*nz_local) periodic
  * box (context created with halo = 1, z0 = r*nz_local) plus a halo plane below and above.  The
- * whole sweep schedule runs in C: interior planes on the context stream, the boundary plane of
- * each colour phase on an auxiliary stream beside it, and only that colour's quarter of the
- * boundary plane sent to the neighbour (RCCL send/recv) while the next interior runs.  Every rank
+ * whole sweep schedule runs in C.  The 8 colour phases of a sweep form runs of equal z parity q (two
+ * runs of 4 with the default order); each run is three independent launch chains: the interior
+ * planes in two chains (context stream and a second stream) and the boundary plane of parity q on
+ * the exchange stream, which then sends that whole plane to the neighbour holding it as a halo and
+ * receives the opposite halo (one RCCL send/recv each way per run) while the interior chains run.
+ * After shiftCells only a z shift needs one more plane (with its counts) from one side.  Every rank
  * derives the sweep plan itself and RNG counters use global cell ids, so any world size
  * reproduces the single-GPU run bit for bit.  librccl is dlopen'ed ("librccl.so.1", or the path
  * in PMC_RCCL_LIB). */
@@ -207,11 +210,13 @@ int pmc_slab_observables(pmc_ctx* ctx, int with_energy, pmc_stats* out, double* 
 /* Sum of the HIP-event durations of the subsweep and shift launches since the last call
  * (synchronizes), then switch per-launch events on (enable = 1) or off.  The events ride on the
  * kernels' own dispatch packets (no extra packets between launches); graph replays and the
- * overflow (fallback) launches are not timed.  pmc_timing reports the subsweep launches on the
- * context stream (the slab driver's interior planes) and the shift launches; pmc_slab_timing is the
- * same call, requiring the slab driver.  pmc_timing_kinds splits by kind: [0] subsweep launches on
- * the context stream, [1] shiftCells, [2] subsweep launches on another stream (the slab driver's
- * boundary planes, which run concurrently with [0]: their durations overlap and do not add). */
+ * overflow (fallback) launches are not timed.  pmc_timing reports the kind-[0] subsweep launches and
+ * the shift launches; pmc_slab_timing is the same call, requiring the slab driver.
+ * pmc_timing_kinds splits by kind: [0] subsweep launches of whole colour phases or of a slab's
+ * interior planes (the slab driver's two interior chains, planes [1, zs) on the context stream and
+ * [zs, nz_local-1) on a second stream, zs = 2*floor(nz_local/4): two launches per phase, running
+ * concurrently), [1] shiftCells, [2] the slab driver's boundary-plane launches and
+ * pmc_phase_range_on launches (other streams: they overlap [0], durations do not add). */
 int pmc_timing(pmc_ctx* ctx, int enable, double* subsweep_ms, int* n_subsweep, double* shift_ms, int* n_shift);
 int pmc_timing_kinds(pmc_ctx* ctx, int enable, double ms[3], int count[3]);
 /* Pause (paused = 1) or resume the per-launch events of pmc_timing without collecting them (no

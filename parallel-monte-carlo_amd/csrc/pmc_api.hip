@@ -49,7 +49,7 @@ struct pmc_ctx {
     bool timing = false;
     bool timing_paused = false;           // pmc_timing_pause: events off without collecting
     std::vector<hipEvent_t> tev;
-    std::vector<int> tkind;                // 0 subsweep (context stream), 1 shift, 2 subsweep (aux stream)
+    std::vector<int> tkind;                // 0 subsweep (interior / context stream), 1 shift, 2 subsweep (boundary / caller stream)
     uint32_t graph_first = 0;
     int graph_count = 0;
     int graph_cur = -1;
@@ -1339,7 +1339,7 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
                 ? launch_subsweep_boundary(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep, c->stats,
                                            ovf, z0, z1, nullptr, 0, st, next_timing(c, 2, &lt))
                 : launch_subsweep(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep, c->stats, ovf, z0,
-                                  z1, st, next_timing(c, kind == kL ? 0 : 2, &lt));
+                                  z1, st, next_timing(c, 0, &lt));   // both interior chains: kind 0
             if (le != hipSuccess) return hip_fail(le, "subsweep launch");
         }
         return PMC_OK;

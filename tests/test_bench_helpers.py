@@ -78,7 +78,49 @@ def test_host_cpu_description():
 
 
 def test_traffic_profile_is_per_launch_json():
-    t = bench.traffic_from_profile()
+    t = bench.traffic_from_profile("3", False, 128)
     assert t is not None, "profiles/pmc_traffic.json is committed with the PMC traffic of the bench kernel"
     assert t["subsweep_bytes_per_launch"] > 0
     assert t["read_bytes_per_launch"] + t["write_bytes_per_launch"] > 0
+
+
+def _gather_rank(rank, world, port, cps, nz, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    plane, row = cps * cps, 3 * 4
+    # rank r's storage: halo, nz owned planes (values encode global plane and slot), halo
+    disk = np.full((nz + 2) * plane * row, -1.0, np.float32)
+    n = np.full((nz + 2) * plane, -1, np.int16)
+    for z in range(nz):
+        zg = rank * nz + z
+        disk[(z + 1) * plane * row:(z + 2) * plane * row] = zg * 1000 + np.arange(plane * row) % 997
+        n[(z + 1) * plane:(z + 2) * plane] = zg
+    out = bench.make_gather(world, rank, plane, nz, row)(disk, n)
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+def test_make_gather_world2_gloo():
+    """bench.py's gather of the owned planes (the N>1 line's CPU baseline and parity leg): rank 0
+    receives the whole box in global plane order, the halo planes dropped; other ranks get None."""
+    import multiprocessing as mp
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    world, cps, nz = 2, 4, 3
+    ps = [ctx.Process(target=_gather_rank, args=(r, world, port, cps, nz, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(60)
+    assert res[1] is None
+    disk, n = res[0]
+    plane, row = cps * cps, 12
+    assert np.array_equal(n, np.repeat(np.arange(world * nz), plane).astype(np.int16))
+    expect = np.concatenate([zg * 1000 + np.arange(plane * row) % 997 for zg in range(world * nz)]).astype(np.float32)
+    assert np.array_equal(disk, expect)

@@ -473,12 +473,11 @@ def test_gpu_c_slab_driver_timing_and_restart(pmc, oracle, tmp_path):
     drv.ctx.slab_timing(True)
     drv.run(0, 2)
     t = drv.ctx.slab_timing(True)
-    assert t["n_subsweep"] == 2 * 8 and t["n_shift"] == 2 and t["subsweep_ms"] > 0 and t["shift_ms"] > 0
+    # nz = 16: per phase one launch of each interior chain (planes [1, 8) and [8, 15))
+    assert t["n_subsweep"] == 2 * 16 and t["n_shift"] == 2 and t["subsweep_ms"] > 0 and t["shift_ms"] > 0
     drv.run(0, 1)
-    k = drv.ctx.timing_kinds(True)   # interior (context stream), shift, boundary (aux stream)
-    # nz = 16: the lower interior chain on the context stream (8 launches), the upper interior chain
-    # and the boundary chain on the other streams (8 each)
-    assert k["n_subsweep"] == 8 and k["n_boundary"] == 16 and k["n_shift"] == 1 and k["boundary_ms"] > 0
+    k = drv.ctx.timing_kinds(True)   # interior (both chains), shift, boundary (exchange stream)
+    assert k["n_subsweep"] == 16 and k["n_boundary"] == 8 and k["n_shift"] == 1 and k["boundary_ms"] > 0
     drv.ctx.slab_timing(False)
     drv = SlabDriver(cps=16, nz_local=16, rank=0, world=1, atoms_per_rank=10_000)
     drv.run(0, 2)
