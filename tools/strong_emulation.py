@@ -40,7 +40,16 @@ def main() -> int:
     ap.add_argument("--p2p", choices=["rccl", "local"], default="rccl")
     ap.add_argument("--driver", choices=["c", "python"], default="c",
                     help="c: the C slab driver (pmc_slab_*, product); python: SlabSimulation")
+    ap.add_argument("--cpus", type=int, default=0,
+                    help="restrict the process (and every thread it starts: HIP runtime, RCCL proxy) to the "
+                         "first N CPUs it may use, before any GPU call -- an 8-GPU node's share per rank "
+                         "(the GPU box's cgroup quota of 16 CPUs / 8 ranks = 2)")
     args = ap.parse_args()
+    cpus_used = None
+    if args.cpus:
+        allowed = sorted(os.sched_getaffinity(0))
+        os.sched_setaffinity(0, allowed[:args.cpus])
+        cpus_used = sorted(os.sched_getaffinity(0))
 
     import torch
     import torch.distributed as dist
@@ -144,7 +153,7 @@ def main() -> int:
            "projected_speedup": t1 / tr, "projected_efficiency": t1 / tr / R,
            "projected_whole_job_trial_moves_per_s": trials_rank * R / tr,
            "host_issue_ms_per_sweep": issue / args.rank_steps * 1e3, "host_only_ms_per_sweep": host_only * 1e3,
-           "error_flags": flags,
+           "error_flags": flags, "cpu_affinity": cpus_used,
            "note": "one GPU running one rank's slab of the config-4 box with the product slab driver; "
                    "excludes xGMI link time and neighbour skew"}
     print(json.dumps(out))
