@@ -27,6 +27,10 @@
 
 namespace pmc {
 
+#ifndef PMC_BITOP3
+#define PMC_BITOP3 0   // Philox key/word xors as one v_bitop3_b32 (A/B)
+#endif
+
 #ifdef PMC_STAMPS
 // Analysis build only (-DPMC_STAMPS, tools/stamps.py): per-wave s_memtime stamps at the section
 // boundaries of a main-launch cell visit, written by lane 0 with vector stores.
@@ -146,8 +150,15 @@ __device__ __forceinline__ pmc_u32x4 philox_sched(uint32_t c0, uint32_t c1, uint
     for (int r = 0; r < 10; ++r) {
         const uint64_t p0 = (uint64_t)PMC_PHILOX_M0 * (uint64_t)c0;
         const uint64_t p1 = (uint64_t)PMC_PHILOX_M1 * (uint64_t)c2;
+#if PMC_BITOP3
+        // gfx950's three-input bitwise op (truth table 0x96 = a ^ b ^ c): one VALU per word
+        uint32_t n0, n2;
+        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n0) : "v"((uint32_t)(p1 >> 32)), "v"(c1), "s"(g.rk0[r]));
+        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n2) : "v"((uint32_t)(p0 >> 32)), "v"(c3), "s"(g.rk1[r]));
+#else
         const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ g.rk0[r];
         const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ g.rk1[r];
+#endif
         c1 = (uint32_t)p1;
         c3 = (uint32_t)p0;
         c0 = n0;
@@ -438,6 +449,11 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
 
     // ---- Fisher-Yates shuffle of the own cell (random_shuffle, subsweep.h:50-58; fixes R1) ---
     int perm;
+#ifdef PMC_PROBE_NO_SHUFFLE   // timing probe only (wrong results): the identity instead of Fisher-Yates
+    if (true) {
+        perm = lane;
+    } else
+#endif
     if (n_own <= 16) {
         // the permutation as 16 nibbles of one 64-bit scalar: each swap is a few SALU ops on
         // SGPRs (no VGPR read-modify-write chain through v_readlane), one VALU unpack at the end
