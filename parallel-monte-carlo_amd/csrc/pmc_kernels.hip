@@ -28,7 +28,7 @@
 namespace pmc {
 
 #ifndef PMC_BITOP3
-#define PMC_BITOP3 0   // Philox key/word xors as one v_bitop3_b32 (A/B)
+#define PMC_BITOP3 1   // Philox key/word xors as one v_bitop3_b32 (sweep -0.3%, profiles/r03h_ab.txt)
 #endif
 
 #ifdef PMC_STAMPS
@@ -265,16 +265,34 @@ struct CellGeo {
     bool edge;
 };
 
+// With zlog, a range whose colour-plane count ncz the group size does not divide ends in a short
+// group of ncz % G planes (same order inside it: x, then its planes, then y).
 __device__ __forceinline__ CellGeo cell_geo(const DevGeom& g, int p, int cz0, int ox, int oy, int oz,
-                                            int zlog = 0) {
+                                            int zlog = 0, int ncz = 0) {
     CellGeo cg;
     const int hx = g.cps_x >> 1, hy = g.cps_y >> 1;
-    const uint32_t q1 = udiv_magic((uint32_t)p, g.div_ncx);     // p / hx
-    const uint32_t q3 = q1 >> zlog;
-    const uint32_t q2 = udiv_magic(q3, g.div_ncy);               // group (plain order: plane)
+    const uint32_t q1 = udiv_magic((uint32_t)p, g.div_ncx);     // p / hx: row of the visiting order
     cg.ta = p - (int)q1 * hx;
-    cg.tb = (int)q3 - (int)q2 * hy;
-    const int tcr = ((int)q2 << zlog) + (int)(q1 & ((1u << zlog) - 1u));   // colour plane in the range
+    int tcr;                                                     // colour plane in the range
+    if (zlog == 0) {
+        const uint32_t q2 = udiv_magic(q1, g.div_ncy);           // plane
+        cg.tb = (int)q1 - (int)q2 * hy;
+        tcr = (int)q2;
+    } else {
+        const uint32_t lim = (uint32_t)(ncz >> zlog) * (uint32_t)hy << zlog;   // rows of the full groups
+        if (q1 < lim) {
+            const uint32_t q3 = q1 >> zlog;
+            const uint32_t q2 = udiv_magic(q3, g.div_ncy);       // group
+            cg.tb = (int)q3 - (int)q2 * hy;
+            tcr = ((int)q2 << zlog) + (int)(q1 & ((1u << zlog) - 1u));
+        } else {                                                 // the short last group: gl planes
+            const uint32_t r = q1 - lim;
+            const uint32_t gl = (uint32_t)ncz & ((1u << zlog) - 1u);   // 1..3 (PMC_ZGROUP <= 4)
+            const uint32_t tb = gl == 1u ? r : (gl == 2u ? r >> 1 : (uint32_t)(((uint64_t)r * 0xAAAAAAABull) >> 33));
+            cg.tb = (int)tb;
+            tcr = ((ncz >> zlog) << zlog) + (int)(r - tb * gl);
+        }
+    }
     cg.t = zlog ? cg.ta + hx * (cg.tb + hy * tcr) : p;
     const int tc = cz0 + tcr;                              // colour plane (z = 2*tc + oz)
     cg.x = 2 * cg.ta + ox;
@@ -813,7 +831,7 @@ __device__ __forceinline__ void subsweep_pair(const DevGeom& g, float* __restric
                                               const int16_t* __restrict__ ncnt, int ox, int oy, int oz,
                                               uint32_t sweep, unsigned long long* __restrict__ stats,
                                               float* __restrict__ px_, int lcap_rt, int cap, int pA, int pB, bool hasB,
-                                              int cz0, int zlog, int* __restrict__ ovf, float* __restrict__ mirror = nullptr,
+                                              int cz0, int zlog, int ncz, int* __restrict__ ovf, float* __restrict__ mirror = nullptr,
                                               int mirror_mode = 0) {
     const int lane = threadIdx.x & (kWave - 1);
     const int nm = NMC > 0 ? NMC : g.nmax;
@@ -825,8 +843,8 @@ __device__ __forceinline__ void subsweep_pair(const DevGeom& g, float* __restric
     float* buf = pz_ + stride;
     const int h = lane & 32;                       // 0: cell A's half, 32: cell B's
     const int l = lane & 31;
-    const CellGeo ca = cell_geo(g, pA, cz0, ox, oy, oz, zlog);
-    const CellGeo cb = cell_geo(g, hasB ? pB : pA, cz0, ox, oy, oz, zlog);
+    const CellGeo ca = cell_geo(g, pA, cz0, ox, oy, oz, zlog, ncz);
+    const CellGeo cb = cell_geo(g, hasB ? pB : pA, cz0, ox, oy, oz, zlog, ncz);
     const int tA = ca.t, tB = cb.t;
     [[maybe_unused]] int t = tA;                   // (PMC_STAMP's cell index)
     PMC_STAMP(0);
@@ -927,9 +945,11 @@ __global__ __launch_bounds__(kWave * kSubWaves) __attribute__((amdgpu_waves_per_
     // 2w and 2w+1 of the visiting order
     const int t = 2 * ((int)b * kSubWaves + wv);
     if (t >= total) return;
-    const int zlog = (ncz & ((1 << kZGroupLog) - 1)) == 0 ? kZGroupLog : 0;
+    // groups of PMC_ZGROUP colour planes, a short last group for a ragged count (PMC_ZGROUP <= 4;
+    // larger groups only for counts they divide)
+    const int zlog = (PMC_ZGROUP <= 4 || (ncz & ((1 << kZGroupLog) - 1)) == 0) ? kZGroupLog : 0;
     subsweep_pair<NSLOT, NMC, kMainCap, OFF32>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, kMainCap, cap, t, t + 1,
-                                               t + 1 < total, cz0, zlog, ovf);
+                                               t + 1 < total, cz0, zlog, ncz, ovf);
 #else
     const int t = (int)b * kSubWaves + wv;
     if (t >= total) return;
