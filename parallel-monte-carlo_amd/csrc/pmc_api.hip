@@ -32,6 +32,7 @@ struct pmc_ctx {
     int cur = 0;
     unsigned long long* stats = nullptr;   // kStatCounters * kStatSlots
     unsigned long long* eacc = nullptr;    // kStatSlots (energy)
+    int* segq = nullptr;                   // energy: queue of row segments over the staging capacity
     uint32_t* flags = nullptr;
     int* ovf = nullptr;                    // subsweep overflow queue (1 + cells per colour)
     int* ovf_aux = nullptr;                // second queue: launches on a caller stream (pmc_phase_range_on)
@@ -275,6 +276,7 @@ void pmc_destroy(pmc_ctx* c) {
     free_state(c);
     if (c->stats) (void)hipFree(c->stats);
     if (c->eacc) (void)hipFree(c->eacc);
+    if (c->segq) (void)hipFree(c->segq);
     if (c->flags) (void)hipFree(c->flags);
     if (c->ovf) (void)hipFree(c->ovf);
     if (c->ovf_aux) (void)hipFree(c->ovf_aux);
@@ -544,7 +546,9 @@ int pmc_run_graph(pmc_ctx* c, uint32_t first, int count) {
 int energy_fixed(pmc_ctx* c, int64_t* fixed) {
     if (int rj = slab_join(c)) return rj;
     PMC_HIP(hipMemsetAsync(c->eacc, 0, sizeof(unsigned long long) * kStatSlots, c->stream));
-    hipError_t e = launch_energy(c->G, c->disk[c->cur], c->n[c->cur], c->eacc, c->stream);
+    if (!c->segq) PMC_HIP(hipMalloc(&c->segq, sizeof(int) * (1 + energy_segments(c->G))));
+    PMC_HIP(hipMemsetAsync(c->segq, 0, sizeof(int), c->stream));
+    hipError_t e = launch_energy(c->G, c->disk[c->cur], c->n[c->cur], c->eacc, c->segq, c->stream);
     if (e != hipSuccess) return hip_fail(e, "energy launch");
     std::vector<unsigned long long> h(kStatSlots);
     PMC_HIP(hipMemcpyAsync(h.data(), c->eacc, sizeof(unsigned long long) * kStatSlots, hipMemcpyDeviceToHost,

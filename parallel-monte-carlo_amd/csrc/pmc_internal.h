@@ -100,8 +100,10 @@ hipError_t launch_shift_planes(const DevGeom& g, const float* din, const int16_t
 hipError_t launch_init_r(const DevGeom& g, int64_t n_atoms, int64_t n_cube, float* r, hipStream_t st);
 hipError_t launch_assign(const DevGeom& g, const float* r, int64_t n_atoms, float* disk, int16_t* n,
                          int32_t* tmp_cnt, int32_t* tmp_idx, uint32_t* flags, hipStream_t st, int clip = 0);
+// segq: int[1 + energy_segments(g)] scratch, zeroed on st before the call
+size_t energy_segments(const DevGeom& g);
 hipError_t launch_energy(const DevGeom& g, const float* disk, const int16_t* n,
-                         unsigned long long* acc, hipStream_t st);
+                         unsigned long long* acc, int* segq, hipStream_t st);
 // the cells of one colour of one plane: mode 0 plane -> packed buffer, 1 packed -> plane,
 // 2 plane -> plane; (cps_x/2)*(cps_y/2)*3*nmax floats
 hipError_t launch_colour_rows(const DevGeom& g, const float* src, float* dst, int colour, int mode, hipStream_t st);

@@ -27,6 +27,9 @@
 
 namespace pmc {
 
+#ifndef PMC_CMPX
+#define PMC_CMPX 0     // term-list compaction with v_cmpx-set exec (A/B)
+#endif
 #ifndef PMC_BITOP3
 #define PMC_BITOP3 1   // Philox key/word xors as one v_bitop3_b32 (sweep -0.3%, profiles/r03h_ab.txt)
 #endif
@@ -78,6 +81,38 @@ __device__ __forceinline__ int mbcnt64_add(unsigned long long m, int add) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, (uint32_t)add));
 }
 __device__ __forceinline__ int mbcnt64(unsigned long long m) { return mbcnt64_add(m, 0); }
+
+// One block's term list (PMC_CMPX): the new-position lanes within the cutoff, then the old-position
+// ones, each compacted by mbcnt over its mask, with exec set by v_cmpx (one VALU writes the mask and
+// exec: no s_and_saveexec / s_or_b64 pair per list) and restored to all lanes (the move loop runs
+// with every lane active).  Same list as the C form below, bit for bit.
+__device__ __forceinline__ void list_block_cmpx(float r2n, float r2on, float rc2, float nrc2, uint32_t lbase,
+                                                int& C) {
+    int t, k;
+    unsigned long long mn, mo;
+    asm volatile(
+        "v_cmpx_ge_f32_e64 %[mn], %[rc2], %[r2n]\n\t"
+        "v_mov_b32 %[t], %[C]\n\t"
+        "v_mbcnt_lo_u32_b32 %[t], exec_lo, %[t]\n\t"
+        "v_mbcnt_hi_u32_b32 %[t], exec_hi, %[t]\n\t"
+        "v_lshl_add_u32 %[t], %[t], 2, %[lb]\n\t"
+        "ds_write_b32 %[t], %[r2n]\n\t"
+        "s_bcnt1_i32_b64 %[k], %[mn]\n\t"
+        "s_add_i32 %[C], %[C], %[k]\n\t"
+        "s_mov_b64 exec, -1\n\t"
+        "v_cmpx_ge_f32_e64 %[mo], %[r2on], %[nrc2]\n\t"
+        "v_mov_b32 %[t], %[C]\n\t"
+        "v_mbcnt_lo_u32_b32 %[t], exec_lo, %[t]\n\t"
+        "v_mbcnt_hi_u32_b32 %[t], exec_hi, %[t]\n\t"
+        "v_lshl_add_u32 %[t], %[t], 2, %[lb]\n\t"
+        "ds_write_b32 %[t], %[r2on]\n\t"
+        "s_bcnt1_i32_b64 %[k], %[mo]\n\t"
+        "s_add_i32 %[C], %[C], %[k]\n\t"
+        "s_mov_b64 exec, -1"
+        : [C] "+s"(C), [t] "=&v"(t), [k] "=&s"(k), [mn] "=&s"(mn), [mo] "=&s"(mo)
+        : [r2n] "v"(r2n), [r2on] "v"(r2on), [rc2] "s"(rc2), [nrc2] "s"(nrc2), [lb] "s"(lbase)
+        : "memory");
+}
 
 // pmc_lj4_signed_m with the r2 floor as ONE v_max_f32 (|r2s| is a free source modifier; the
 // compiler's fmaxf would add canonicalizing maxes, the C form a compare + select): identical
@@ -442,6 +477,8 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
     float* py_ = px_ + stride;
     float* pz_ = py_ + stride;
     float* buf = pz_ + stride;                  // term list: signed r2 values
+    [[maybe_unused]] const uint32_t buf_off = (uint32_t)wave_uniform((int)(uint32_t)(uintptr_t)(
+        const __attribute__((address_space(3))) char*)buf);   // LDS byte address (PMC_CMPX)
     const int ta = cg.ta, tb = cg.tb, x = cg.x, y = cg.y, zg0 = cg.zg0;
     const uint32_t c = cg.c, id = cg.id;
     const bool edge = cg.edge;
@@ -672,7 +709,12 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
                     const float xj = px_[k], yj = py_[k], zj = pz_[k];
                     // old-position term computed negated (= -r2o bit for bit, pmc_r2_neg):
                     // listed with its sign bit set at no extra instruction
+#if PMC_CMPX
+                    list_block_cmpx(pmc_r2(qx - xj, qy - yj, qz - zj), pmc_r2_neg(xi - xj, yi - yj, zi - zj),
+                                    rc2, nrc2, buf_off, C);
+#else
                     list(pmc_r2(qx - xj, qy - yj, qz - zj), pmc_r2_neg(xi - xj, yi - yj, zi - zj));
+#endif
                 };
                 if constexpr (NB > 0) {
 #pragma unroll
@@ -1355,10 +1397,34 @@ constexpr int kEnergyCells = PMC_ENERGY_CELLS;
 #endif
 constexpr int kEnergyRing = PMC_ENERGY_STEP == 2 ? 256 : 128;
 
-template <int NSLOT, bool OFF32>
+// k_energy_rows: one wave per row segment of kESeg cells along x; the 9 neighbouring rows of the
+// segment (kESeg + 2 cells each) are staged once, kECap particles at most
+constexpr int kESeg = 8;
+constexpr int kERows = 5;                   // the rows of an interior cell's half shell
+constexpr int kEStaged = kERows * (kESeg + 2);   // staged cells per segment (< 64: one lane each)
+static_assert(kEStaged < 64, "one lane per staged cell");
+constexpr int kECap = 384;                  // staged particles (4.77 per cell: ~240; near-lattice states +4.5 sd)
+constexpr int kEList = 14 * 16;             // a cell's filtered partner list (indices into the staging)
+
+// A cell is an "edge" cell for the energy when a stencil neighbour is wrapped across the periodic
+// box or lies in a halo plane (slab mode): its pairs with that neighbour are directed (weight 1,
+// evaluated from each side).  Every other cell's neighbours are all mutual, and k_energy_rows takes
+// it (half shell, weight 2).
+__device__ __forceinline__ bool energy_edge_cell(const DevGeom& g, int x, int y, int zl) {
+    const int zg = g.z0 + zl;
+    return x == 0 || x == g.cps_x - 1 || y == 0 || y == g.cps_y - 1 || zg == 0 || zg == g.cps_z - 1 ||
+           (g.halo && (zl == 0 || zl == g.nz_local - 1));
+}
+
+// Cell-list energy, one wave per group of cells.  MODE 0: every owned cell, kEnergyCells
+// consecutive cells per wave; 1: only the edge cells among them (k_energy_rows takes the rest);
+// 2: the interior cells of the row segments k_energy_rows could not stage (its queue `segq`:
+// [0] count, then segment ids), a fixed grid striding over the queue.
+template <int NSLOT, bool OFF32, int MODE>
 __global__ __launch_bounds__(kWave) void k_energy(DevGeom g, const float* __restrict__ disk,
                                                   const int16_t* __restrict__ ncnt,
-                                                  unsigned long long* __restrict__ acc, uint32_t total_cells) {
+                                                  unsigned long long* __restrict__ acc, uint32_t total_cells,
+                                                  const int* __restrict__ segq, UDivMagic div_nsx) {
     extern __shared__ __attribute__((aligned(16))) float esm[];
     constexpr int HS = NSLOT >= 16 ? 8 : NSLOT;       // staging lanes per cell (slots [0, HS))
     constexpr int CPP = kWave / HS;                   // cells per staging pass
@@ -1377,8 +1443,18 @@ __global__ __launch_bounds__(kWave) void k_energy(DevGeom g, const float* __rest
     const float r2min = g.r2min;
     long long sum = 0;
 
-    const uint32_t t0 = blockIdx.x * (uint32_t)kEnergyCells;
-    const int ncl = (int)(total_cells - t0 < (uint32_t)kEnergyCells ? total_cells - t0 : (uint32_t)kEnergyCells);
+    // cells of this wave: base + the set bits of `todo` (ascending)
+    auto cell_xyz = [&](uint32_t t, int* x, int* y, int* zl) {
+        const uint32_t q1 = udiv_magic(t, g.div_cx);
+        const uint32_t zq = udiv_magic(t, g.div_plane);
+        *x = (int)(t - q1 * (uint32_t)g.cps_x);
+        *zl = (int)zq;
+        *y = (int)(q1 - zq * (uint32_t)g.cps_y);
+    };
+    const EnergyLaneConst lc = energy_lane_const(g);
+    // the wave's cells: ncl of them, pop() returns the next cell id (wave-uniform)
+    auto run_cells = [&](int ncl, auto pop) {
+    if (ncl == 0) return;
     // staged-cell list of the cell whose rows are in flight: entry -> stencil lane in inv_l,
     // its group masks; rows in registers
     float vx[NPMAX], vy[NPMAX], vz[NPMAX];
@@ -1424,11 +1500,10 @@ __global__ __launch_bounds__(kWave) void k_energy(DevGeom g, const float* __rest
         }
     };
 
-    const EnergyLaneConst lc = energy_lane_const(g);
-    EnergyStencil cur = energy_stencil(g, ncnt, t0, lc);
+    EnergyStencil cur = energy_stencil(g, ncnt, pop(), lc);
     issue_rows(cur);
     EnergyStencil nxt = cur;
-    if (ncl > 1) nxt = energy_stencil(g, ncnt, t0 + 1, lc);
+    if (ncl > 1) nxt = energy_stencil(g, ncnt, pop(), lc);
     for (int c = 0; c < ncl; ++c) {
         // ---- stage cell c from the rows in registers: own cell (all slots), weight-2 cells,
         //      then weight-1 cells (each group: main slots, then the fuller cells' slots [HS, n))
@@ -1501,7 +1576,7 @@ __global__ __launch_bounds__(kWave) void k_energy(DevGeom g, const float* __rest
         if (c + 1 < ncl) {
             cur = nxt;
             issue_rows(cur);
-            if (c + 2 < ncl) nxt = energy_stencil(g, ncnt, t0 + (uint32_t)c + 2u, lc);
+            if (c + 2 < ncl) nxt = energy_stencil(g, ncnt, pop(), lc);
         }
         if (n_own == 0) continue;
         // ---- pairs (i, j): lane j holds staged partner j (blocks of 64), own particle i < n_own
@@ -1576,10 +1651,239 @@ __global__ __launch_bounds__(kWave) void k_energy(DevGeom g, const float* __rest
 #endif
         if (C > 0) drain(C);
     }
+    };   // run_cells
+    if constexpr (MODE == 2) {
+        // queued row segments (k_energy_rows): their interior cells, kESeg consecutive cells in x
+        const int nq = __builtin_amdgcn_readfirstlane(segq[0]);
+        for (int k = (int)blockIdx.x; k < nq; k += (int)gridDim.x) {
+            const uint32_t seg = (uint32_t)__builtin_amdgcn_readfirstlane(segq[1 + k]);
+            const uint32_t row = udiv_magic(seg, div_nsx);
+            const uint32_t x0 = (seg - row * (uint32_t)((g.cps_x + kESeg - 1) / kESeg)) * (uint32_t)kESeg;
+            const uint32_t base = row * (uint32_t)g.cps_x + x0;
+            int x, y, zl;
+            cell_xyz(base + (uint32_t)lane, &x, &y, &zl);
+            unsigned long long todo = __builtin_amdgcn_ballot_w64(lane < kESeg && x0 + (uint32_t)lane < (uint32_t)g.cps_x &&
+                                                                  !energy_edge_cell(g, x, y, zl));
+            run_cells(__popcll(todo), [&]() -> uint32_t {
+                const int b = (int)__builtin_ctzll(todo);
+                todo &= todo - 1ull;
+                return base + (uint32_t)b;
+            });
+        }
+    } else if constexpr (MODE == 1) {
+        // the edge cells, enumerated densely: planes zl = 0 and nz-1 whole, then per middle plane
+        // the rows y = 0 and cps_y-1 and the cells x = 0 and cps_x-1 of the rows between
+        const uint32_t P = (uint32_t)g.cps_x * (uint32_t)g.cps_y;
+        const uint32_t M = 2u * (uint32_t)g.cps_x + 2u * (uint32_t)(g.cps_y - 2);
+        const uint32_t k0 = blockIdx.x * (uint32_t)kEnergyCells;
+        const int ncl = (int)(total_cells - k0 < (uint32_t)kEnergyCells ? total_cells - k0 : (uint32_t)kEnergyCells);
+        uint32_t k = k0;
+        run_cells(ncl, [&]() -> uint32_t {
+            const uint32_t kk = k++;
+            uint32_t zl, x, y;
+            if (kk < 2u * P) {
+                zl = kk < P ? 0u : (uint32_t)g.nz_local - 1u;
+                const uint32_t tin = kk < P ? kk : kk - P;
+                y = udiv_magic(tin, g.div_cx);
+                x = tin - y * (uint32_t)g.cps_x;
+            } else {
+                const uint32_t k1 = kk - 2u * P;
+                const uint32_t pl = k1 / M;                        // (SALU: once per cell)
+                const uint32_t r = k1 - pl * M;
+                zl = 1u + pl;
+                if (r < 2u * (uint32_t)g.cps_x) {
+                    y = r < (uint32_t)g.cps_x ? 0u : (uint32_t)g.cps_y - 1u;
+                    x = r < (uint32_t)g.cps_x ? r : r - (uint32_t)g.cps_x;
+                } else {
+                    const uint32_t r2 = r - 2u * (uint32_t)g.cps_x;
+                    y = 1u + (r2 >> 1);
+                    x = (r2 & 1u) ? (uint32_t)g.cps_x - 1u : 0u;
+                }
+            }
+            return x + (uint32_t)g.cps_x * (y + (uint32_t)g.cps_y * zl);
+        });
+    } else {
+        const uint32_t t0 = blockIdx.x * (uint32_t)kEnergyCells;
+        const int ncl = (int)(total_cells - t0 < (uint32_t)kEnergyCells ? total_cells - t0 : (uint32_t)kEnergyCells);
+        uint32_t t = t0;
+        run_cells(ncl, [&]() -> uint32_t { return t++; });
+    }
     // wave sum (int64, exact in any order), one atomic per wave
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
-    if (lane == 0) atomicAdd(&acc[blockIdx.x & (kStatSlots - 1)], (unsigned long long)sum);
+    if (lane == 0 && sum != 0) atomicAdd(&acc[blockIdx.x & (kStatSlots - 1)], (unsigned long long)sum);
+}
+
+// Cell-list energy of the interior cells (no wrapped or halo neighbour: every pair mutual), one wave
+// per row segment of kESeg cells along x.  An interior cell's half shell lies in five rows: its own
+// row (the cell and its +x neighbour) and the rows (y+1, z), (y-1..y+1, z+1) (cells x-1..x+1).  These
+// five rows over x0-1 .. x0+SL are staged ONCE for the segment: counts first, their exclusive prefix
+// gives every staged cell its start in LDS, then the rows go straight to those starts (no
+// compaction, no image: an interior cell's neighbours are never wrapped).  Per own cell the half
+// shell is five contiguous staged ranges, walked as one flattened index and filtered through the
+// own cell's box (pmc_box_d2, as the subsweep: a dropped partner's energy is exactly 0) into a
+// partner list, own particles first (own-own pairs j > i).  Every pair is mutual, weight 2 (the
+// oracle's two directed terms are the same bits); the fixed-point terms are summed in int64, exact in
+// any order, so interior + edge cells (k_energy MODE 1) + queued segments (MODE 2) equal orc_energy
+// bit for bit.  A segment holding more than `cap` particles is queued for MODE 2.
+template <int NSLOT, bool OFF32>
+__global__ __launch_bounds__(kWave) void k_energy_rows(DevGeom g, const float* __restrict__ disk,
+                                                       const int16_t* __restrict__ ncnt,
+                                                       unsigned long long* __restrict__ acc, int* __restrict__ segq,
+                                                       UDivMagic div_nsx, UDivMagic div_cy, int cap) {
+    extern __shared__ __attribute__((aligned(16))) float rsm[];
+    float* ex_ = rsm;
+    float* ey_ = rsm + kECap;
+    float* ez_ = rsm + 2 * kECap;
+    float* ring = rsm + 3 * kECap;                    // listed pairs (signed r2), kEnergyRing
+    int* lst = (int*)(ring + kEnergyRing);            // the own cell's partners (staged indices)
+    int2* rec = (int2*)(lst + kEList);                // staged cell: storage index, start | count << 16
+    const int lane = threadIdx.x;
+    const int nm = g.nmax;
+    const int nsx = (g.cps_x + kESeg - 1) / kESeg;
+    const uint32_t seg = blockIdx.x;
+    const uint32_t row = udiv_magic(seg, div_nsx);    // y + cps_y * zl
+    const int x0 = (int)(seg - row * (uint32_t)nsx) * kESeg;
+    const uint32_t zq = udiv_magic(row, div_cy);
+    const int zl = (int)zq, y = (int)(row - zq * (uint32_t)g.cps_y);
+    const int zg = g.z0 + zl;
+    // a segment on a y or z face (or next to a halo plane) holds edge cells only: k_energy MODE 1
+    if (y == 0 || y == g.cps_y - 1 || zg == 0 || zg == g.cps_z - 1 || (g.halo && (zl == 0 || zl == g.nz_local - 1)))
+        return;
+    const int SL = g.cps_x - x0 < kESeg ? g.cps_x - x0 : kESeg;
+    const int W = SL + 2, E = kERows * W;             // E < 64: one lane per staged cell
+    // ---- staged cell e = r*W + q (lane e): row r in {(0,0), (+1,0), (-1,+1), (0,+1), (+1,+1)} as
+    //      (dy, dz), cell x = x0 - 1 + q; cells outside [0, cps_x) neighbour edge cells only: not
+    //      staged (count 0)
+    const int r = (int)(((uint32_t)lane * ((65536u + (uint32_t)W - 1u) / (uint32_t)W)) >> 16);   // lane / W
+    const int q = lane - r * W;
+    const int dy = ((585 >> (2 * r)) & 3) - 1, dz = r >= 2 ? 1 : 0;
+    const int xs = x0 - 1 + q;
+    const bool st = lane < E && xs >= 0 && xs < g.cps_x;
+    const int sidx = st ? xs + g.cps_x * (y + dy + g.cps_y * (zl + dz + g.halo)) : 0;
+    const int cnt = st ? (int)ncnt[sidx] : 0;
+    int inc = cnt;                                    // inclusive prefix of the counts over e
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int u = __shfl_up(inc, (unsigned)d);
+        inc += lane >= d ? u : 0;
+    }
+    const int total = __builtin_amdgcn_readlane(inc, 63);
+    // (never at equilibrium densities; nmax > 16: a cell's 14-cell list could exceed kEList)
+    if (total > cap || 14 * nm > kEList) {   // the per-cell kernel (MODE 2) takes the segment
+        if (lane == 0) segq[1 + atomicAdd(&segq[0], 1)] = (int)seg;
+        return;
+    }
+    const int start = inc - cnt;                      // lane E: the total
+    rec[lane] = make_int2(sidx, start | (cnt << 16));
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    // ---- stage: slots [0, HS) of CPP cells per pass, then the fuller cells' slots [HS, n)
+    constexpr int HS = NSLOT >= 16 ? 8 : NSLOT;
+    constexpr int CPP = kWave / HS;
+    using DA = DiskAddr<OFF32>;
+    const int p = lane % HS, ce = lane / HS;
+    const uint32_t nmu = (uint32_t)nm * DA::kUnit;
+    for (int e0 = 0; e0 < E; e0 += CPP) {
+        const int e = e0 + ce;
+        const int2 rc = rec[e < E ? e : E];
+        const int c_n = rc.y >> 16, c_s = rc.y & 0xffff;
+        if (e < E && p < c_n) {
+            const uint32_t off = ((uint32_t)rc.x * (uint32_t)(3 * nm) + (uint32_t)p) * DA::kUnit;
+            ex_[c_s + p] = DA::ld(disk, off);
+            ey_[c_s + p] = DA::ld(disk, off + nmu);
+            ez_[c_s + p] = DA::ld(disk, off + 2u * nmu);
+        }
+    }
+    if constexpr (HS < NSLOT) {
+        unsigned long long ov = __builtin_amdgcn_ballot_w64(cnt > HS);
+        while (ov) {
+            int ks = 0, nc = 0;
+            for (; nc < CPP && ov; ++nc) {
+                const int kb = (int)__builtin_ctzll(ov);
+                ov &= ov - 1ull;
+                ks = ce == nc ? kb : ks;
+            }
+            const int2 rc = rec[ks];
+            const int c_n = rc.y >> 16, c_s = rc.y & 0xffff;
+            for (int ps = HS + p; ps < NSLOT; ps += HS) {
+                if (ce < nc && ps < c_n) {
+                    const uint32_t off = ((uint32_t)rc.x * (uint32_t)(3 * nm) + (uint32_t)ps) * DA::kUnit;
+                    ex_[c_s + ps] = DA::ld(disk, off);
+                    ey_[c_s + ps] = DA::ld(disk, off + nmu);
+                    ez_[c_s + ps] = DA::ld(disk, off + 2u * nmu);
+                }
+            }
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    // staged cell e's start (e <= E) as a scalar
+    auto st_of = [&](int e) -> int { return __builtin_amdgcn_readlane(start, e); };
+    const float rc2 = g.rc2, r2min = g.r2min;
+    long long sum = 0;
+    constexpr int RM = kEnergyRing - 1;
+    for (int s = 0; s < SL; ++s) {
+        const int x = x0 + s;
+        if (x == 0 || x == g.cps_x - 1) continue;       // edge cell (MODE 1)
+        const int eo = s + 1;                            // own cell: row 0
+        const int sA = st_of(eo), sA1 = st_of(eo + 1), eA = st_of(eo + 2);
+        const int n_own = sA1 - sA;
+        if (n_own == 0) continue;
+        // ranges: A = own cell + its +x neighbour; B..E = cells x-1..x+1 of rows 1..4
+        const int sB = st_of(W + s), eB = st_of(W + s + 3);
+        const int sC = st_of(2 * W + s), eC = st_of(2 * W + s + 3);
+        const int sD = st_of(3 * W + s), eD = st_of(3 * W + s + 3);
+        const int sE = st_of(4 * W + s), eE = st_of(4 * W + s + 3);
+        const int P1 = eA - sA, P2 = P1 + (eB - sB), P3 = P2 + (eC - sC), P4 = P3 + (eD - sD);
+        const int T = P4 + (eE - sE);
+        // the partner list: own particles first (unfiltered: the j > i pairs), then the others
+        // within the cutoff of the own cell's (padded) box
+        float blo[3], bhi[3];
+        pmc_cell_box(x, y, zg, g.w, g.Lx, g.Ly, g.Lz, blo, bhi);
+        if (lane < n_own) lst[lane] = sA + lane;
+        int S = n_own;
+        for (int jb = 0; jb < T; jb += kWave) {
+            const int j = jb + lane;
+            const int src = j < P1 ? sA + j : (j < P2 ? sB + (j - P1) : (j < P3 ? sC + (j - P2) :
+                            (j < P4 ? sD + (j - P3) : sE + (j - P4))));
+            const int sj = j < T ? src : 0;
+            const bool keep = j >= n_own && j < T && pmc_box_d2(ex_[sj], ey_[sj], ez_[sj], blo, bhi) <= g.rc2f;
+            const unsigned long long mk = __builtin_amdgcn_ballot_w64(keep);
+            if (keep) lst[S + mbcnt64(mk)] = sj;
+            S += __popcll(mk);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        const float ox = lane < n_own ? ex_[sA + lane] : 0.0f;
+        const float oy = lane < n_own ? ey_[sA + lane] : 0.0f;
+        const float oz = lane < n_own ? ez_[sA + lane] : 0.0f;
+        int head = 0, C = 0;
+        auto drain = [&](int lim) {
+            if (lane < lim) sum += energy_term(ring[(head + lane) & RM], r2min);
+            head = (head + 64) & RM;
+            C -= lim;
+        };
+        for (int jb = 0; jb < S; jb += kWave) {
+            const int j = jb + lane;
+            const int sj = lst[j < S ? j : 0];
+            const float xj = ex_[sj], yj = ey_[sj], zj = ez_[sj];
+            unsigned long long vm = __builtin_amdgcn_ballot_w64(j < S);
+            for (int i = 0; i < n_own; ++i) {
+                const float xi = as_f(__builtin_amdgcn_readlane(as_i(ox), i));
+                const float yi = as_f(__builtin_amdgcn_readlane(as_i(oy), i));
+                const float zi = as_f(__builtin_amdgcn_readlane(as_i(oz), i));
+                const float r2 = pmc_r2(xi - xj, yi - yj, zi - zj);
+                if (jb == 0) vm &= vm - 1ull;             // own slots j <= i: lanes 0..i of block 0
+                const unsigned long long im = __builtin_amdgcn_ballot_w64(r2 <= rc2) & vm;
+                if (__builtin_amdgcn_inverse_ballot_w64(im))
+                    ring[(head + C + mbcnt64(im)) & RM] = as_f(as_i(r2) | (int)0x80000000);   // weight 2
+                C += __popcll(im);
+                if (C >= 64) drain(64);
+            }
+        }
+        if (C > 0) drain(C);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+    if (lane == 0 && sum != 0) atomicAdd(&acc[blockIdx.x & (kStatSlots - 1)], (unsigned long long)sum);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1826,8 +2130,15 @@ hipError_t launch_assign(const DevGeom& g, const float* r, int64_t n_atoms, floa
     return hipGetLastError();
 }
 
+size_t energy_segments(const DevGeom& g) {
+    return (size_t)((g.cps_x + kESeg - 1) / kESeg) * (size_t)g.cps_y * (size_t)g.nz_local;
+}
+
+// segq: int[1 + energy_segments(g)], zeroed by the caller before the launches (on st).  Interior
+// cells by row segments (k_energy_rows), edge cells (k_energy MODE 1), then the segments the rows
+// kernel queued (MODE 2, normally none).  PMC_ENERGY_LEGACY=1: MODE 0 alone (every cell per cell).
 hipError_t launch_energy(const DevGeom& g, const float* disk, const int16_t* n,
-                         unsigned long long* acc, hipStream_t st) {
+                         unsigned long long* acc, int* segq, hipStream_t st) {
     const int64_t total = (int64_t)g.cps_x * g.cps_y * g.nz_local;   // owned cells
     const size_t lds = sizeof(float) * (3 * 27 * (size_t)g.nmax + kEnergyRing + 32);
     dim3 grid((unsigned)((total + kEnergyCells - 1) / kEnergyCells)), block(kWave);
@@ -1835,13 +2146,42 @@ hipError_t launch_energy(const DevGeom& g, const float* disk, const int16_t* n,
     // 32-bit byte offsets below 4 GiB of disk (every single-GPU 256^3 box), else element offsets
     const int64_t bytes = (int64_t)g.cps_x * g.cps_y * (g.nz_local + 2 * g.halo) * 3 * g.nmax * 4;
     const bool off32 = bytes < ((int64_t)1 << 32);
-    auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, block, lds, st, g, disk, n, acc, tc); };
+    static const bool legacy = [] {
+        const char* v = std::getenv("PMC_ENERGY_LEGACY");
+        return v && std::atoi(v) == 1;
+    }();
+    // test hook: PMC_ENERGY_ROWS_CAP lowers the staging capacity (0: every segment queued, MODE 2)
+    static const int cap = [] {
+        const char* v = std::getenv("PMC_ENERGY_ROWS_CAP");
+        const int k = v ? std::atoi(v) : kECap;
+        return k < 0 ? 0 : (k > kECap ? kECap : k);
+    }();
+    const int nsx = (g.cps_x + kESeg - 1) / kESeg;
+    const UDivMagic div_nsx = make_udiv_magic((uint32_t)nsx), div_cy = make_udiv_magic((uint32_t)g.cps_y);
+    // edge cells (energy_edge_cell): planes 0 and nz_local-1 whole, the rim of every plane between
+    // (every plane's first and last plane coincide with the slab's halo-neighbour or box-face planes)
+    const int64_t n_edge = 2 * (int64_t)g.cps_x * g.cps_y +
+                           (int64_t)(g.nz_local - 2) * (2 * (int64_t)g.cps_x + 2 * (int64_t)(g.cps_y - 2));
+    const size_t lds_rows = sizeof(float) * (3 * kECap + kEnergyRing) + sizeof(int) * kEList + sizeof(int2) * 64;
+    const dim3 grid_rows((unsigned)energy_segments(g));
+    auto go = [&](auto k0, auto k1, auto k2, auto kr) {
+        if (legacy) {
+            hipLaunchKernelGGL(k0, grid, block, lds, st, g, disk, n, acc, tc, segq, div_nsx);
+            return;
+        }
+        hipLaunchKernelGGL(kr, grid_rows, block, lds_rows, st, g, disk, n, acc, segq, div_nsx, div_cy, cap);
+        hipLaunchKernelGGL(k1, dim3((unsigned)((n_edge + kEnergyCells - 1) / kEnergyCells)), block, lds, st, g, disk, n,
+                           acc, (uint32_t)n_edge, segq, div_nsx);
+        hipLaunchKernelGGL(k2, dim3(64), block, lds, st, g, disk, n, acc, tc, segq, div_nsx);
+    };
+#define PMC_ENERGY_GO(NS, O32) go(k_energy<NS, O32, 0>, k_energy<NS, O32, 1>, k_energy<NS, O32, 2>, k_energy_rows<NS, O32>)
     switch (g.nslot) {
-        case 8: off32 ? go(k_energy<8, true>) : go(k_energy<8, false>); break;
-        case 16: off32 ? go(k_energy<16, true>) : go(k_energy<16, false>); break;
-        case 32: off32 ? go(k_energy<32, true>) : go(k_energy<32, false>); break;
-        default: off32 ? go(k_energy<64, true>) : go(k_energy<64, false>); break;
+        case 8: off32 ? PMC_ENERGY_GO(8, true) : PMC_ENERGY_GO(8, false); break;
+        case 16: off32 ? PMC_ENERGY_GO(16, true) : PMC_ENERGY_GO(16, false); break;
+        case 32: off32 ? PMC_ENERGY_GO(32, true) : PMC_ENERGY_GO(32, false); break;
+        default: off32 ? PMC_ENERGY_GO(64, true) : PMC_ENERGY_GO(64, false); break;
     }
+#undef PMC_ENERGY_GO
     return hipGetLastError();
 }
 

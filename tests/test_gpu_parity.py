@@ -336,6 +336,47 @@ print("ok", r["accepted"])
     assert out.stdout.startswith("ok")
 
 
+@pytest.mark.parametrize("env", [{"PMC_ENERGY_ROWS_CAP": "0"}, {"PMC_ENERGY_ROWS_CAP": "40"},
+                                 {"PMC_ENERGY_LEGACY": "1"}])
+def test_energy_paths_equal_oracle(oracle, env):
+    """The cell-list energy's launch variants, each bitwise equal to orc_energy: interior cells by
+    row segments + edge cells per cell (default); every segment over a tiny staging capacity, so the
+    per-cell kernel takes the queued segments (ROWS_CAP 0 / 40); the per-cell kernel alone (LEGACY).
+    Whole boxes (16^3, 20x12x14) and a slab with halos.  Subprocess: the hooks are read once."""
+    import os
+    import subprocess
+    import sys
+    code = r'''
+import sys, numpy as np
+sys.path[:0] = [sys.argv[1], sys.argv[2]]
+import pmc_amd, pmc_oracle
+for cps, cy, cz, atoms in ((16, 16, 16, 10000), (20, 12, 14, 9000), (8, 8, 8, 1500)):
+    ctx = pmc_amd.PmcContext(cps, cps_y=cy, cps_z=cz)
+    ctx.init_lattice(atoms)
+    ctx.start(0, 2)
+    st = pmc_oracle.OracleState(pmc_oracle.make_params(cps=cps, cps_y=cy, cps_z=cz))
+    disk, n = ctx.copy_out()
+    st.disk[:] = disk; st.n[:] = n
+    assert ctx.energy() == st.energy(), (cps, ctx.energy(), st.energy())
+# slab with halo planes: the slab's energy equals the oracle's over the same storage
+from pmc_amd.slab import SlabDriver
+d = SlabDriver(cps=16, nz_local=8, rank=0, world=1, atoms_per_rank=5000, use_rccl=False)
+d.run(3, 2)
+e = d.ctx.energy()
+disk, n = d.ctx.copy_out()
+stp = pmc_oracle.OracleState(pmc_oracle.make_params(cps=16, cps_z=8, nz_local=8, halo=1))
+stp.disk[:] = disk; stp.n[:] = n
+assert e == stp.energy(), (e, stp.energy())
+print("ok")
+'''
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", code, os.path.join(repo, "parallel-monte-carlo_amd"),
+                          os.path.join(repo, "oracle")], env=dict(os.environ, **env),
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "ok" in out.stdout
+
+
 @pytest.mark.parametrize("rccl", [False, True])
 def test_gpu_c_slab_driver_forced_fallback(rccl):
     """PMC_SUBSWEEP_CAP=64 sends (almost) every cell of the C slab driver's interior launches to

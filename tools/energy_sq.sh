@@ -1,20 +1,8 @@
 #!/bin/bash
-# SQ instruction mix and wait cycles of k_energy (tools/energy_timing.py, 128^3 / 1e7).
-# Usage (GPU box, repo root): bash tools/energy_sq.sh <tag>
+# SQ instruction mix and wave cycles of the energy kernels (tools/energy_timing.py workload), one
+# rocprofv3 --pmc pass.  Usage (GPU box): bash tools/energy_sq.sh <tag>
 set -o pipefail
-OUT=gpurun_out/esq_$1; mkdir -p $OUT
+O=gpurun_out/esq_$1; mkdir -p $O
 export TMPDIR=/tmp
-timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY -T --output-format csv -d $OUT/p1 -o run -- python3 tools/energy_timing.py > $OUT/p1.log 2>&1 || exit $?
-timeout -s KILL 180 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_VALU_CVT SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 GRBM_GUI_ACTIVE -T --output-format csv -d $OUT/p2 -o run -- python3 tools/energy_timing.py > $OUT/p2.log 2>&1 || exit $?
-python3 - "$OUT" <<'PY'
-import csv, glob, sys, collections
-agg = collections.defaultdict(float); n = collections.defaultdict(set)
-for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
-    for r in csv.DictReader(open(f)):
-        if "k_energy" in r["Kernel_Name"]:
-            agg[r["Counter_Name"]] += float(r["Counter_Value"]); n[r["Counter_Name"]].add((f, r["Dispatch_Id"]))
-cells = 128 ** 3
-for c in sorted(agg):
-    m = agg[c] / len(n[c])
-    print(f"{c:24s} per dispatch {m:14.1f}  per cell {m / cells:9.2f}")
-PY
+timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d $O/p -o run -- python3 tools/energy_timing.py > $O/run.log 2>&1 || { tail -5 $O/run.log; exit 1; }
+python3 tools/pmc_summary.py $O/p | grep k_energy
