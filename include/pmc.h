@@ -239,6 +239,14 @@ int pmc_start_ex(pmc_ctx* ctx, uint32_t first_sweep, int mc_passes, int flags, p
 /* Record the sweep loop (pmc_sweep for sweeps first..first+count-1) as a hipGraph and
  * replay it; identical results to calling pmc_sweep in a loop. */
 int pmc_run_graph(pmc_ctx* ctx, uint32_t first_sweep, int count);
+/* Small boxes (whole box, nmax 16, at most 2048 cells per colour, e.g. 16^3): sweeps
+ * first..first+count-1 as ONE launch per 32 sweeps on one XCD, in-kernel barriers where the 17
+ * launches of a sweep were (start.cu:242-249's per-phase launch + synchronize); identical results
+ * to pmc_sweep in a loop.  PMC_ERR_ARG for a box that does not qualify.  One XCD is an eighth of the
+ * chip: faster than per-phase launches only for tiny boxes, so pmc_start uses it for boxes of at
+ * most 64 cells per colour (PMC_SMALL=0 in the environment: never).  Error flags bit 3: a
+ * barrier timed out; bit 4: a participant ran outside XCD 0. */
+int pmc_run_small(pmc_ctx* ctx, uint32_t first_sweep, int count);
 
 /* ---- observables ------------------------------------------------------------------- */
 /* Total LJ energy of the owned cells' particles (calc_energy, kernel.cu:452-470, as an
@@ -246,7 +254,8 @@ int pmc_run_graph(pmc_ctx* ctx, uint32_t first_sweep, int count);
 int pmc_energy(pmc_ctx* ctx, double* e_out);
 /* Read and optionally reset the accumulated subsweep statistics (synchronises). */
 int pmc_stats_read(pmc_ctx* ctx, pmc_stats* out, int reset);
-/* Device error flags (bit 0: shift overflow, bit 1: assign overflow, bit 2: assign range);
+/* Device error flags (bit 0: shift overflow, bit 1: assign overflow, bit 2: assign range, bits 3-4:
+ * pmc_run_small);
  * synchronises; `reset` clears them. */
 int pmc_error_flags(pmc_ctx* ctx, uint32_t* flags, int reset);
 

@@ -598,6 +598,31 @@ int pmc_error_flags(pmc_ctx* c, uint32_t* flags, int reset) {
     return PMC_OK;
 }
 
+int pmc_run_small(pmc_ctx* c, uint32_t first, int count) {
+    if (!c || count < 0) return fail(PMC_ERR_ARG, "bad argument");
+    if (small_sweep_participants(c->G) == 0)
+        return fail(PMC_ERR_ARG, "pmc_run_small: the box does not qualify (whole box, nmax 16, <= 2048 cells per colour)");
+    if (count == 0) return PMC_OK;
+    // barrier counter: flags word 2 (word 0 holds the error bits)
+    hipError_t e = launch_sweep_small(c->G, c->disk[0], c->n[0], c->disk[1], c->n[1], c->cur, c->stats, c->flags,
+                                      (unsigned*)(c->flags + 2), c->P.seed, first, count, c->P.flags, c->stream);
+    if (e != hipSuccess) return hip_fail(e, "small-box sweep launch");
+    if (count & 1) c->cur ^= 1;
+    return PMC_OK;
+}
+
+// pmc_start runs the boxes where one launch on XCD 0 beats 17 launches over the 8 XCDs through
+// pmc_run_small: at most 64 cells per colour (8^3: 0.115 against 0.124 ms per sweep; at 16^3 one
+// XCD is 4x slower than the whole chip, profiles/r03n_small_box.txt).  PMC_SMALL=0: never.
+static bool use_small(const pmc_ctx* c) {
+    static const bool off = [] {
+        const char* v = std::getenv("PMC_SMALL");
+        return v && std::atoi(v) == 0;
+    }();
+    const int64_t per_colour = (int64_t)(c->P.cps_x / 2) * (c->P.cps_y / 2) * (c->P.cps_z / 2);
+    return !off && small_sweep_participants(c->G) > 0 && per_colour <= 64;
+}
+
 int pmc_start_ex(pmc_ctx* c, uint32_t first, int mc_passes, int flags, pmc_result* out) {
     if (!c || mc_passes < 0) return fail(PMC_ERR_ARG, "bad argument");
     if (c->P.halo) return fail(PMC_ERR_ARG, "pmc_start drives the whole box; use the slab driver for halo mode");
@@ -610,9 +635,13 @@ int pmc_start_ex(pmc_ctx* c, uint32_t first, int mc_passes, int flags, pmc_resul
     if (rc) return rc;
     if (energies && (rc = pmc_energy(c, &r.e_initial))) return rc;
     PMC_HIP(hipEventRecord(c->ev0, c->stream));
-    for (int k = 0; k < mc_passes; ++k) {
-        rc = enqueue_sweep(c, first + (uint32_t)k);
-        if (rc) return rc;
+    if (use_small(c) && !c->timing) {
+        if ((rc = pmc_run_small(c, first, mc_passes))) return rc;
+    } else {
+        for (int k = 0; k < mc_passes; ++k) {
+            rc = enqueue_sweep(c, first + (uint32_t)k);
+            if (rc) return rc;
+        }
     }
     PMC_HIP(hipEventRecord(c->ev1, c->stream));
     PMC_HIP(hipEventSynchronize(c->ev1));
@@ -633,6 +662,8 @@ int pmc_start_ex(pmc_ctx* c, uint32_t first, int mc_passes, int flags, pmc_resul
     if (rc) return rc;
     if (out) *out = r;
     if (fl & 1u) return fail(PMC_ERR_OVERFLOW, "shiftCells: cell occupancy exceeded nmax");
+    if (fl & 8u) return fail(PMC_ERR_HIP, "small-box sweep: a barrier timed out (participants not co-resident)");
+    if (fl & 16u) return fail(PMC_ERR_HIP, "small-box sweep: a participant ran outside XCD 0");
     return PMC_OK;
 }
 

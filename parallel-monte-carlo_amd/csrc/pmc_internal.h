@@ -90,6 +90,13 @@ hipError_t launch_subsweep_boundary(const DevGeom& g, float* disk, const int16_t
                                     float* mirror, int mirror_mode, hipStream_t st,
                                     const LaunchTiming* tm = nullptr);
 int subsweep_capacity(const DevGeom& g);
+// whole sweeps of a small whole box in one launch on XCD 0 (k_sweep_small); bar: one unsigned of
+// scratch; cur: the current buffer of the (disk, n) pairs; returns hipErrorInvalidValue when the box
+// does not qualify (small_sweep_participants == 0)
+int small_sweep_participants(const DevGeom& g);
+hipError_t launch_sweep_small(const DevGeom& g, float* disk0, int16_t* n0, float* disk1, int16_t* n1, int cur,
+                              unsigned long long* stats, uint32_t* flags, unsigned* bar, uint64_t seed,
+                              uint32_t first, int count, uint32_t plan_flags, hipStream_t st);
 hipError_t launch_shift(const DevGeom& g, const float* din, const int16_t* nin, float* dout,
                         int16_t* nout, int f, float d, uint32_t* flags, hipStream_t st,
                         const LaunchTiming* tm = nullptr);

@@ -20,6 +20,7 @@
 #include <hip/hip_ext.h>
 
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 #include "pmc_internal.h"
@@ -1070,6 +1071,160 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_fallback(DevGeom
 }
 
 // ------------------------------------------------------------------------------------------
+// Small boxes: whole sweeps in ONE launch on ONE XCD (pmc_run_small).
+//
+// At 16^3 a colour phase is 512 cells: a sweep of 17 launches is dispatch-bound (~7.5 us each for
+// a few us of work).  This kernel runs `count` sweeps (8 colour phases + shiftCells each) with P
+// persistent one-wave workgroups and an in-kernel barrier where each kernel boundary was.  The
+// launch has 8*P workgroups; workgroup b runs on XCD b % 8 (tools/ubench/xcc_map.hip: 4096 of
+// 4096), and only those with b % 8 == 0 stay: all P participants then share XCD 0's L2, which is the
+// coherence point for them -- a barrier needs no L2 write-back, only (a) its stores completed
+// (s_waitcnt vmcnt(0): the vector L1 is write-through), (b) an L2 atomic, (c) the vector L1
+// invalidated afterwards (buffer_inv sc1; no buffer_wbl2).  (A grid barrier across the 8 XCDs must write back and
+// invalidate each L2 -- round 2 measured that 3-6x slower than eager launches.)  A participant that
+// finds itself on another XCD flags error bit 4 (the results would not be coherent).  Every cell
+// visit uses the full-capacity LDS layout (27*nmax partners: no overflow queue), 9.9 KB per wave,
+// 16 waves per CU: XCD 0 holds 512 participants.  Barrier waits give up after ~1 s of s_memrealtime
+// (error bit 8) so a participant that never arrives cannot hang the GPU.
+// ------------------------------------------------------------------------------------------
+constexpr int kSmallSweeps = 32;   // sweep plans per launch
+struct SmallPlans {
+    int n;                          // sweeps in this launch
+    uint32_t first;                 // sweep index of the first
+    int order[kSmallSweeps][8];     // colour order
+    int f[kSmallSweeps];            // shift axis
+    float d[kSmallSweeps];          // shift distance
+};
+
+__device__ __forceinline__ bool small_barrier(unsigned* bar, unsigned target, uint32_t* flags) {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    if ((threadIdx.x & (kWave - 1)) == 0) __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();        // 100 MHz
+    bool ok = true;
+    while (true) {
+        const unsigned v = __builtin_amdgcn_readfirstlane(
+            (int)__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));   // L1 bypass, XCD 0's L2
+        if ((int)(v - target) >= 0) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 100000000ull) {
+            ok = false;
+            if ((threadIdx.x & (kWave - 1)) == 0) atomicOr(flags, 8u);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    // vector L1: drop stale lines.  (sc0, workgroup scope, is a no-op outside threadgroup-split
+    // mode -- 8^3 read stale neighbour rows with it; sc1, agent scope, invalidates the L1 and only
+    // MTYPE NC lines of the L2, none of which hipMalloc memory has.)
+    asm volatile("buffer_inv sc1" ::: "memory");
+    return ok;
+}
+
+// shiftCells of cells [c0, c0 + 64/NSLOT) (one cell per NSLOT-lane group), the arithmetic of k_shift
+// (shiftCells.h:46-108, float s of the fixed copy) for one cell per lane group
+template <int NSLOT>
+__device__ __forceinline__ void shift_cells_wave(const DevGeom& g, const float* __restrict__ din,
+                                                 const int16_t* __restrict__ nin, float* __restrict__ dout,
+                                                 int16_t* __restrict__ nout, int f, float d, uint32_t* __restrict__ flags,
+                                                 int c0, int ncells) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int p = lane & (NSLOT - 1);
+    const int ci = c0 + lane / NSLOT;
+    const bool live = ci < ncells;
+    const int c = live ? ci : 0;
+    const int nm = g.nmax;
+    const float w = g.w;
+    const int cps_f = f == 0 ? g.cps_x : (f == 1 ? g.cps_y : g.cps_z);
+    const float Lf = f == 0 ? g.Lx : (f == 1 ? g.Ly : g.Lz);
+    const int dir = (d <= 0) ? -1 : 1;
+    const float s = w * (float)dir;
+    const int x = c % g.cps_x, y = (c / g.cps_x) % g.cps_y, z = c / (g.cps_x * g.cps_y);
+    const int cidf = f == 0 ? x : (f == 1 ? y : z);
+    const float offset = (float)cidf * w - Lf / 2.0f;
+    int nbg = cidf + dir;
+    if (nbg < 0) nbg = cps_f - 1; else if (nbg >= cps_f) nbg = 0;
+    const int nx = f == 0 ? nbg : x, ny = f == 1 ? nbg : y, nz = f == 2 ? nbg : z;
+    const float offset_nb = (float)nbg * w - Lf / 2.0f;
+    const int cnb = nx + g.cps_x * (ny + g.cps_y * nz);
+    const int ncur = live ? (int)nin[c] : 0, nnb = live ? (int)nin[cnb] : 0;
+    const int pp = p < nm ? p : 0;
+    float own[3], nbv[3];
+#pragma unroll
+    for (int dim = 0; dim < 3; ++dim) {
+        own[dim] = din[(uint64_t)c * (uint64_t)(3 * nm) + (uint64_t)(dim * nm + pp)];
+        nbv[dim] = din[(uint64_t)cnb * (uint64_t)(3 * nm) + (uint64_t)(dim * nm + pp)];
+    }
+    const int gsh = lane & ~(NSLOT - 1);
+    const unsigned long long gmask = NSLOT == 64 ? ~0ull : ((1ull << (NSLOT & 63)) - 1ull);
+    const unsigned long long below = (1ull << p) - 1ull;
+    const float xf = f == 0 ? own[0] : (f == 1 ? own[1] : own[2]);
+    const float xfn = f == 0 ? nbv[0] : (f == 1 ? nbv[1] : nbv[2]);
+    const float D = (xf - offset) - d;
+    const float Dn = (xfn - offset_nb) - d;
+    const bool keep = (p < ncur) && (D > 0 && D <= w);
+    const bool take = (p < nnb) && !(Dn > 0 && Dn <= w);
+    const unsigned long long km = (__ballot(keep) >> gsh) & gmask;
+    const unsigned long long tm = (__ballot(take) >> gsh) & gmask;
+    const int nk = __popcll(km);
+    const int nnew = nk + __popcll(tm);
+    const uint64_t ob = (uint64_t)c * (uint64_t)(3 * nm);
+    if (keep) {
+        const int dst = __popcll(km & below);
+        if (dst < nm)
+#pragma unroll
+            for (int dim = 0; dim < 3; ++dim) dout[ob + (uint64_t)(dim * nm + dst)] = (dim == f) ? D + offset : own[dim];
+    }
+    if (take) {
+        const int dst = nk + __popcll(tm & below);
+        if (dst < nm)
+#pragma unroll
+            for (int dim = 0; dim < 3; ++dim)
+                dout[ob + (uint64_t)(dim * nm + dst)] = (dim == f) ? ((Dn + offset) + s) : nbv[dim];
+    }
+    if (live && p == 0) {
+        nout[c] = (int16_t)(nnew > nm ? nm : nnew);
+        if (nnew > nm) atomicOr(flags, 1u);
+    }
+}
+
+template <int NSLOT, int NMC, bool OFF32>
+__global__ __launch_bounds__(kWave) void k_sweep_small(DevGeom g, float* __restrict__ disk0, int16_t* __restrict__ n0,
+                                                      float* __restrict__ disk1, int16_t* __restrict__ n1,
+                                                      unsigned long long* __restrict__ stats, uint32_t* __restrict__ flags,
+                                                      unsigned* __restrict__ bar, SmallPlans plans) {
+    if (blockIdx.x & 7u) return;                      // not on XCD 0
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    if ((xcc & 0xFu) != 0u && (threadIdx.x & (kWave - 1)) == 0) atomicOr(flags, 16u);
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    constexpr int full = 27 * NMC;
+    const int P = (int)(gridDim.x >> 3), pid = (int)(blockIdx.x >> 3);
+    const int per_colour = (g.cps_x >> 1) * (g.cps_y >> 1) * (g.cps_z >> 1);
+    const int cells = g.cps_x * g.cps_y * g.cps_z;
+    unsigned target = 0;
+    float* dk[2] = {disk0, disk1};
+    int16_t* nk[2] = {n0, n1};
+    int cur = 0;
+    for (int k = 0; k < plans.n; ++k) {
+        const uint32_t sweep = plans.first + (uint32_t)k;
+        for (int ph = 0; ph < 8; ++ph) {
+            int o[3];
+            pmc_colour_offset(plans.order[k][ph], o);
+            for (int t = pid; t < per_colour; t += P)
+                (void)subsweep_wave<NSLOT, NMC, full, OFF32>(g, dk[cur], nk[cur], o[0], o[1], o[2], sweep, stats, smem,
+                                                             full, full, t, 0);
+            target += (unsigned)P;
+            if (!small_barrier(bar, target, flags)) return;
+        }
+        constexpr int CPW = kWave / NSLOT;
+        for (int c0 = pid * CPW; c0 < cells; c0 += P * CPW)
+            shift_cells_wave<NSLOT>(g, dk[cur], nk[cur], dk[cur ^ 1], nk[cur ^ 1], plans.f[k], plans.d[k], flags, c0, cells);
+        target += (unsigned)P;
+        if (!small_barrier(bar, target, flags)) return;
+        cur ^= 1;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // shiftCells: NSLOT lanes per cell, ballot compaction (shiftCells.h:28-144; float s of the fixed
 // copy CUDA-Parallel-MC/CUDA-Parallel-MC/shiftCells.h:23-112).  Double-buffered.
 // ------------------------------------------------------------------------------------------
@@ -2077,6 +2232,49 @@ hipError_t launch_subsweep(const DevGeom& g, float* disk, const int16_t* n, int 
     if (!force64 && bytes < ((int64_t)1 << 32)) launch_subsweep_n<true>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st, tm);
     else launch_subsweep_n<false>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st, tm);
     return hipGetLastError();
+}
+
+// Participants of k_sweep_small for a box (0: the box does not qualify -- nmax != 16, a slab, or
+// a colour phase over 4 cells per participant).  XCD 0 holds 512 waves of the 9.9 KB layout.
+int small_sweep_participants(const DevGeom& g) {
+    if (g.nmax != 16 || g.halo) return 0;
+    const int64_t per_colour = (int64_t)(g.cps_x / 2) * (g.cps_y / 2) * (g.cps_z / 2);
+    if (per_colour > 4 * 512) return 0;
+    return per_colour < 512 ? (int)per_colour : 512;
+}
+
+hipError_t launch_sweep_small(const DevGeom& g, float* disk0, int16_t* n0, float* disk1, int16_t* n1, int cur,
+                              unsigned long long* stats, uint32_t* flags, unsigned* bar, uint64_t seed,
+                              uint32_t first, int count, uint32_t plan_flags, hipStream_t st) {
+    const int P = small_sweep_participants(g);
+    if (P == 0) return hipErrorInvalidValue;
+    const size_t lds = sizeof(float) * (size_t)lds_floats_per_wave(27 * 16);
+    const bool off32 = (int64_t)g.cps_x * g.cps_y * g.cps_z * 3 * g.nmax * 4 < ((int64_t)1 << 32);
+    if (!off32) return hipErrorInvalidValue;
+    for (int done = 0; done < count;) {
+        SmallPlans sp;
+        std::memset(&sp, 0, sizeof(sp));
+        sp.n = count - done < kSmallSweeps ? count - done : kSmallSweeps;
+        sp.first = first + (uint32_t)done;
+        for (int k = 0; k < sp.n; ++k) {
+            const pmc_sweep_plan_t plan = pmc_plan_for_sweep_ex(seed, sp.first + (uint32_t)k, g.w, plan_flags);
+            for (int c = 0; c < 8; ++c) sp.order[k][c] = plan.order[c];
+            sp.f[k] = plan.f;
+            sp.d[k] = plan.d;
+        }
+        hipError_t e = hipMemsetAsync(bar, 0, sizeof(unsigned), st);
+        if (e != hipSuccess) return e;
+        float* d0 = cur == 0 ? disk0 : disk1;
+        float* d1 = cur == 0 ? disk1 : disk0;
+        int16_t* m0 = cur == 0 ? n0 : n1;
+        int16_t* m1 = cur == 0 ? n1 : n0;
+        hipLaunchKernelGGL((k_sweep_small<16, 16, true>), dim3(8u * (unsigned)P), dim3(kWave), lds, st, g, d0, m0, d1,
+                           m1, stats, flags, bar, sp);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if (sp.n & 1) cur ^= 1;
+        done += sp.n;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_shift(const DevGeom& g, const float* din, const int16_t* nin, float* dout,

@@ -129,6 +129,7 @@ def lib():
         _sig(L, "pmc_start", i32, _vp, u32, i32, C.POINTER(Result))
         _sig(L, "pmc_start_ex", i32, _vp, u32, i32, i32, C.POINTER(Result))
         _sig(L, "pmc_run_graph", i32, _vp, u32, i32)
+        _sig(L, "pmc_run_small", i32, _vp, u32, i32)
         _sig(L, "pmc_sweep_plan", i32, C.c_uint64, u32, C.c_float, C.POINTER(C.c_int * 8), C.POINTER(C.c_int),
              C.POINTER(C.c_float))
         _sig(L, "pmc_sweep_plan_ex", i32, C.c_uint64, u32, C.c_float, u32, C.POINTER(C.c_int * 8),

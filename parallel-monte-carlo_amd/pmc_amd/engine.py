@@ -236,6 +236,10 @@ class PmcContext:
         out.update(e_initial=r.e_initial, e_final=r.e_final, seconds=r.seconds, sweeps=int(r.sweeps))
         return out
 
+    def run_small(self, first: int, count: int) -> None:
+        """pmc_run_small: whole sweeps of a small box in one launch on one XCD."""
+        check("pmc_run_small", lib().pmc_run_small(self._h, first, count))
+
     def run_graph(self, first: int, count: int) -> None:
         check("pmc_run_graph", lib().pmc_run_graph(self._h, first, count))
 

@@ -236,6 +236,25 @@ def test_graph_replay_equals_oracle(pmc, oracle):
     assert a.stats() == b.stats()
 
 
+@pytest.mark.parametrize("cps,atoms", [((16, 16, 16), 10_000), ((8, 8, 8), 1_500), ((12, 8, 6), 1_800),
+                                       ((20, 20, 20), 24_000), ((24, 24, 24), 40_000)])
+def test_small_box_persistent_equals_oracle(pmc, oracle, cps, atoms):
+    """pmc_run_small (whole sweeps in one launch on XCD 0, in-kernel barriers) equals the oracle bit
+    for bit over 40 sweeps (two launches of 32 + 8), 512 participants looping over up to 4 cells per
+    colour phase at 24^3; pmc_start takes the same path for these boxes."""
+    cx, cy, cz = cps
+    ctx = _ctx(pmc, cx, cps_y=cy, cps_z=cz)
+    ctx.init_lattice(atoms)
+    ctx.run_small(7, 40)
+    st = _ostate(oracle, cx, cps_y=cy, cps_z=cz)
+    st.init_lattice(atoms)
+    assert st.run(7, 40) == 0
+    _assert_same(oracle, ctx, st, 16)
+    assert ctx.stats() == st.stats.as_dict()
+    assert ctx.error_flags() == 0
+    assert ctx.energy() == st.energy()
+
+
 def test_single_colour_parity_64(pmc, oracle):
     """BASELINE config 2: 64^3 cells, 1e6 particles, one colour phase."""
     ctx = _ctx(pmc, 64)
