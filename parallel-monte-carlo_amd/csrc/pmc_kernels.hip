@@ -28,6 +28,9 @@
 
 namespace pmc {
 
+#ifndef PMC_SHIFT_XCD
+#define PMC_SHIFT_XCD 0   // shiftCells blocks in XCD-contiguous order (A/B)
+#endif
 #ifndef PMC_CMPX
 #define PMC_CMPX 0     // term-list compaction with v_cmpx-set exec (A/B)
 #endif
@@ -1246,7 +1249,21 @@ __global__ __launch_bounds__(kShiftThreads) void k_shift(DevGeom g, const float*
     constexpr int CPB = kShiftThreads / NSLOT;
     const int lane = threadIdx.x & (kWave - 1);
     const int p = threadIdx.x & (NSLOT - 1);
+#if PMC_SHIFT_XCD
+    // 1-D grid in XCD-contiguous order: block b runs on XCD b % 8, so XCD k takes rows
+    // [k*R/8, (k+1)*R/8) of the (x-block, y, plane) order and the neighbour rows a shift along y or
+    // z reads are mostly ones its own L2 just fetched (speed only)
+    const uint32_t gx = (uint32_t)((g.cps_x + CPB * U - 1) / (CPB * U));
+    uint32_t lb = blockIdx.x;
+    const uint32_t nblk = gridDim.x;
+    if ((nblk & 7u) == 0u) lb = (lb & 7u) * (nblk >> 3) + (lb >> 3);
+    const uint32_t rowid = lb / gx;
+    const int bx = (int)(lb - rowid * gx);
+    const int y = (int)(rowid % (uint32_t)g.cps_y), zl = zl0 + (int)(rowid / (uint32_t)g.cps_y);
+#else
+    const int bx = (int)blockIdx.x;
     const int y = (int)blockIdx.y, zl = zl0 + (int)blockIdx.z;
+#endif
     const int nm = g.nmax;
     const float w = g.w;
     const int cps_f = f == 0 ? g.cps_x : (f == 1 ? g.cps_y : g.cps_z);
@@ -1265,7 +1282,7 @@ __global__ __launch_bounds__(kShiftThreads) void k_shift(DevGeom g, const float*
     float offset[U], offset_nb[U], own[U][3], nbv[U][3];
 #pragma unroll
     for (int j = 0; j < U; ++j) {
-        const int x = ((int)blockIdx.x * U + j) * CPB + (int)(threadIdx.x / NSLOT);
+        const int x = (bx * U + j) * CPB + (int)(threadIdx.x / NSLOT);
         live[j] = x < g.cps_x;
         const int xx = live[j] ? x : 0;
         int cidf = f == 0 ? xx : (f == 1 ? y : g.z0 + zl);
@@ -2295,8 +2312,12 @@ hipError_t launch_shift_planes(const DevGeom& g, const float* din, const int16_t
 #endif
     constexpr int U = PMC_SHIFT_U;   // cells per lane group, loads hoisted
     const int cpb = kShiftThreads / g.nslot;
+#if PMC_SHIFT_XCD
+    dim3 grid((unsigned)(((g.cps_x + cpb * U - 1) / (cpb * U)) * g.cps_y * (zl_end - zl_begin))), block(kShiftThreads);
+#else
     dim3 grid((unsigned)((g.cps_x + cpb * U - 1) / (cpb * U)), (unsigned)g.cps_y, (unsigned)(zl_end - zl_begin)),
         block(kShiftThreads);
+#endif
     const int z0 = zl_begin;
     switch (g.nslot) {
         case 8: launch_k(k_shift<8, U>, grid, block, 0, st, tm, g, din, nin, dout, nout, f, d, flags, z0); break;
