@@ -245,7 +245,7 @@ int pmc_run_graph(pmc_ctx* ctx, uint32_t first_sweep, int count);
  * to pmc_sweep in a loop.  PMC_ERR_ARG for a box that does not qualify.  One XCD is an eighth of the
  * chip: faster than per-phase launches only for tiny boxes, so pmc_start uses it for boxes of at
  * most 64 cells per colour (PMC_SMALL=0 in the environment: never).  Error flags bit 3: a
- * barrier timed out; bit 4: a participant ran outside XCD 0. */
+ * barrier timed out; bit 4: the launch's blocks were not dealt round-robin over the XCDs. */
 int pmc_run_small(pmc_ctx* ctx, uint32_t first_sweep, int count);
 
 /* ---- observables ------------------------------------------------------------------- */

@@ -663,7 +663,7 @@ int pmc_start_ex(pmc_ctx* c, uint32_t first, int mc_passes, int flags, pmc_resul
     if (out) *out = r;
     if (fl & 1u) return fail(PMC_ERR_OVERFLOW, "shiftCells: cell occupancy exceeded nmax");
     if (fl & 8u) return fail(PMC_ERR_HIP, "small-box sweep: a barrier timed out (participants not co-resident)");
-    if (fl & 16u) return fail(PMC_ERR_HIP, "small-box sweep: a participant ran outside XCD 0");
+    if (fl & 16u) return fail(PMC_ERR_HIP, "small-box sweep: the launch was not dealt round-robin over the XCDs");
     return PMC_OK;
 }
 

@@ -1079,13 +1079,13 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_fallback(DevGeom
 // At 16^3 a colour phase is 512 cells: a sweep of 17 launches is dispatch-bound (~7.5 us each for
 // a few us of work).  This kernel runs `count` sweeps (8 colour phases + shiftCells each) with P
 // persistent one-wave workgroups and an in-kernel barrier where each kernel boundary was.  The
-// launch has 8*P workgroups; workgroup b runs on XCD b % 8 (tools/ubench/xcc_map.hip: 4096 of
-// 4096), and only those with b % 8 == 0 stay: all P participants then share XCD 0's L2, which is the
+// launch has 8*P workgroups dealt round-robin over the 8 XCDs (tools/ubench/xcc_map.hip), and only
+// those the XCC_ID register puts on XCD 0 stay: all P participants then share XCD 0's L2, which is the
 // coherence point for them -- a barrier needs no L2 write-back, only (a) its stores completed
 // (s_waitcnt vmcnt(0): the vector L1 is write-through), (b) an L2 atomic, (c) the vector L1
 // invalidated afterwards (buffer_inv sc1; no buffer_wbl2).  (A grid barrier across the 8 XCDs must write back and
-// invalidate each L2 -- round 2 measured that 3-6x slower than eager launches.)  A participant that
-// finds itself on another XCD flags error bit 4 (the results would not be coherent).  Every cell
+// invalidate each L2 -- round 2 measured that 3-6x slower than eager launches.)  More than P
+// blocks on XCD 0 (a dispatch that is not round-robin) flags error bit 4.  Every cell
 // visit uses the full-capacity LDS layout (27*nmax partners: no overflow queue), 9.9 KB per wave,
 // 16 waves per CU: XCD 0 holds 512 participants.  Barrier waits give up after ~1 s of s_memrealtime
 // (error bit 8) so a participant that never arrives cannot hang the GPU.
@@ -1194,10 +1194,16 @@ __global__ __launch_bounds__(kWave) void k_sweep_small(DevGeom g, float* __restr
                                                       float* __restrict__ disk1, int16_t* __restrict__ n1,
                                                       unsigned long long* __restrict__ stats, uint32_t* __restrict__ flags,
                                                       unsigned* __restrict__ bar, SmallPlans plans) {
-    if (blockIdx.x & 7u) return;                      // not on XCD 0
+    // the dispatcher deals workgroups round-robin over the 8 XCDs, but from wherever the previous
+    // launch left off: participate by the XCC_ID register, not by b % 8.  Consecutive blocks of one
+    // XCD are 8 apart, so b / 8 numbers XCD 0's blocks 0..P-1.
     unsigned xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    if ((xcc & 0xFu) != 0u && (threadIdx.x & (kWave - 1)) == 0) atomicOr(flags, 16u);
+    if ((xcc & 0xFu) != 0u) return;
+    if ((int)(blockIdx.x >> 3) >= (int)(gridDim.x >> 3)) {   // (a 9th block on XCD 0: mapping broken)
+        if ((threadIdx.x & (kWave - 1)) == 0) atomicOr(flags, 16u);
+        return;
+    }
     extern __shared__ __attribute__((aligned(16))) float smem[];
     constexpr int full = 27 * NMC;
     const int P = (int)(gridDim.x >> 3), pid = (int)(blockIdx.x >> 3);
