@@ -185,16 +185,22 @@ static void subsweep_cell(const pmc_params* p, float* disk, const int16_t* n, in
         int t = perm[i]; perm[i] = perm[j]; perm[j] = t;
     }
 
-    /* stage the 26 neighbour cells (get_neighbors order, subsweep.h:119-137; global reads of
+    /* stage the own cell in shuffled order (cpy_to_Dsh, subsweep.h:18-27) into slots [0, n_own),
+     * then the 26 neighbour cells (get_neighbors order, subsweep.h:119-137; global reads of
      * calculate_energy_in_neighbors :153-172 done once, Version II ldisk staging kernel.cu:269-278),
      * keeping only partners within the cutoff of the own cell's box (their pair energy is
-     * otherwise exactly 0); then the own cell in shuffled order (cpy_to_Dsh, subsweep.h:18-27). */
+     * otherwise exactly 0).  Spec v11: own cell first (v10 staged it after the neighbours). */
+    for (int s = 0; s < n_own; ++s) {
+        px_[s] = disk[c * 3 * nm + perm[s]] + 0.0f;
+        py_[s] = disk[c * 3 * nm + nm + perm[s]] + 0.0f;
+        pz_[s] = disk[c * 3 * nm + 2 * nm + perm[s]] + 0.0f;
+    }
     int off[27][3];
     stencil_offsets(off);
     float lo[3], hi[3];
     pmc_cell_box(x, y, p->z0 + zl, p->w, Lx, Ly, Lz, lo, hi);
     const float rcf = pmc_filter_r2(rc2);
-    int S = 0;
+    int S = n_own;
     /* staging order (pmc_stage_split): slots [0, H) of every neighbour in stencil order, then
      * slots [H, n) of the neighbours holding more than H particles, in stencil order */
     const int H = pmc_stage_split(nm);
@@ -215,13 +221,7 @@ static void subsweep_cell(const pmc_params* p, float* disk, const int16_t* n, in
             }
         }
     }
-    const int S_nb = S;
-    for (int s = 0; s < n_own; ++s) {
-        px_[S_nb + s] = disk[c * 3 * nm + perm[s]] + 0.0f;
-        py_[S_nb + s] = disk[c * 3 * nm + nm + perm[s]] + 0.0f;
-        pz_[S_nb + s] = disk[c * 3 * nm + 2 * nm + perm[s]] + 0.0f;
-    }
-    const int K = S_nb + n_own;
+    const int K = S;
 
     /* cell centre (out_of_bound, subsweep.h:73-88): c*w - L/2 + w/2 in float */
     const float hw = p->w / 2.0f;
@@ -238,7 +238,7 @@ static void subsweep_cell(const pmc_params* p, float* disk, const int16_t* n, in
         pmc_move_normals(wm, &g0, &g1, &g2);
         pmc_u32x4 wa = pmc_philox4x32_10((uint32_t)m, id, sweep, PMC_TAG_ACCEPT, k0, k1);
         float T = pmc_accept_threshold(wa);
-        float xi = px_[S_nb + i], yi = py_[S_nb + i], zi = pz_[S_nb + i];
+        float xi = px_[i], yi = py_[i], zi = pz_[i];
         float qx = xi + g0 * p->sigma;
         float qy = yi + g1 * p->sigma;
         float qz = zi + g2 * p->sigma;
@@ -249,7 +249,7 @@ static void subsweep_cell(const pmc_params* p, float* disk, const int16_t* n, in
             ++*ev;
             /* energies (calculate_old/new_energy, subsweep.h:175-191): dE = sum over partners
              * k != i of e(new) - e(old).  Term list (the kernel's compaction, spec v6): for each
-             * block of 64 staged partners (neighbours first, own cell after) append the new
+             * block of 64 staged partners (own cell first, neighbours after) append the new
              * terms with r2 <= rc2 in ascending k, then the old terms with r2 <= rc2 in
              * ascending k (pairs beyond the cutoff are exactly 0 and are not listed).  Term t is
              * summed by lane t%64 in ascending t as +u (new) / -u (old), u the quarter energy;
@@ -262,7 +262,7 @@ static void subsweep_cell(const pmc_params* p, float* disk, const int16_t* n, in
                 for (int pass = 0; pass < 2; ++pass) {
                     const float sx = pass ? xi : qx, sy = pass ? yi : qy, sz = pass ? zi : qz;
                     for (int k = base; k < kend; ++k) {
-                        if (k == S_nb + i) continue;
+                        if (k == i) continue;
                         const float r2 = pmc_r2(sx - px_[k], sy - py_[k], sz - pz_[k]);
                         if (r2 <= rc2) {
                             part[t & 63] = part[t & 63] + pmc_lj4_signed(pass ? -r2 : r2);
@@ -281,7 +281,7 @@ static void subsweep_cell(const pmc_params* p, float* disk, const int16_t* n, in
             const float dE = lane[0];
             /* accept_move (subsweep.h:209-216) as beta*dE < -log(u) */
             if ((double)p->beta * (double)dE < (double)T) {
-                px_[S_nb + i] = qx; py_[S_nb + i] = qy; pz_[S_nb + i] = qz;   /* :219-223 */
+                px_[i] = qx; py_[i] = qy; pz_[i] = qz;   /* :219-223 */
                 ++*acc;
                 de_cell = de_cell + (double)dE;
             }
@@ -292,9 +292,9 @@ static void subsweep_cell(const pmc_params* p, float* disk, const int16_t* n, in
     *de += pmc_to_fixed(de_cell);
     /* cpy_D_sh_to_Disk (subsweep.h:29-36): write back in shuffled order */
     for (int s = 0; s < n_own; ++s) {
-        disk[c * 3 * nm + s] = px_[S_nb + s];
-        disk[c * 3 * nm + nm + s] = py_[S_nb + s];
-        disk[c * 3 * nm + 2 * nm + s] = pz_[S_nb + s];
+        disk[c * 3 * nm + s] = px_[s];
+        disk[c * 3 * nm + nm + s] = py_[s];
+        disk[c * 3 * nm + 2 * nm + s] = pz_[s];
     }
 }
 

@@ -31,9 +31,6 @@ namespace pmc {
 #ifndef PMC_SHIFT_XCD
 #define PMC_SHIFT_XCD 0   // shiftCells blocks in XCD-contiguous order (A/B)
 #endif
-#ifndef PMC_CMPX
-#define PMC_CMPX 0     // term-list compaction with v_cmpx-set exec (A/B)
-#endif
 #ifndef PMC_BITOP3
 #define PMC_BITOP3 1   // Philox key/word xors as one v_bitop3_b32 (sweep -0.3%, profiles/r03h_ab.txt)
 #endif
@@ -85,38 +82,6 @@ __device__ __forceinline__ int mbcnt64_add(unsigned long long m, int add) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, (uint32_t)add));
 }
 __device__ __forceinline__ int mbcnt64(unsigned long long m) { return mbcnt64_add(m, 0); }
-
-// One block's term list (PMC_CMPX): the new-position lanes within the cutoff, then the old-position
-// ones, each compacted by mbcnt over its mask, with exec set by v_cmpx (one VALU writes the mask and
-// exec: no s_and_saveexec / s_or_b64 pair per list) and restored to all lanes (the move loop runs
-// with every lane active).  Same list as the C form below, bit for bit.
-__device__ __forceinline__ void list_block_cmpx(float r2n, float r2on, float rc2, float nrc2, uint32_t lbase,
-                                                int& C) {
-    int t, k;
-    unsigned long long mn, mo;
-    asm volatile(
-        "v_cmpx_ge_f32_e64 %[mn], %[rc2], %[r2n]\n\t"
-        "v_mov_b32 %[t], %[C]\n\t"
-        "v_mbcnt_lo_u32_b32 %[t], exec_lo, %[t]\n\t"
-        "v_mbcnt_hi_u32_b32 %[t], exec_hi, %[t]\n\t"
-        "v_lshl_add_u32 %[t], %[t], 2, %[lb]\n\t"
-        "ds_write_b32 %[t], %[r2n]\n\t"
-        "s_bcnt1_i32_b64 %[k], %[mn]\n\t"
-        "s_add_i32 %[C], %[C], %[k]\n\t"
-        "s_mov_b64 exec, -1\n\t"
-        "v_cmpx_ge_f32_e64 %[mo], %[r2on], %[nrc2]\n\t"
-        "v_mov_b32 %[t], %[C]\n\t"
-        "v_mbcnt_lo_u32_b32 %[t], exec_lo, %[t]\n\t"
-        "v_mbcnt_hi_u32_b32 %[t], exec_hi, %[t]\n\t"
-        "v_lshl_add_u32 %[t], %[t], 2, %[lb]\n\t"
-        "ds_write_b32 %[t], %[r2on]\n\t"
-        "s_bcnt1_i32_b64 %[k], %[mo]\n\t"
-        "s_add_i32 %[C], %[C], %[k]\n\t"
-        "s_mov_b64 exec, -1"
-        : [C] "+s"(C), [t] "=&v"(t), [k] "=&s"(k), [mn] "=&s"(mn), [mo] "=&s"(mo)
-        : [r2n] "v"(r2n), [r2on] "v"(r2on), [rc2] "s"(rc2), [nrc2] "s"(nrc2), [lb] "s"(lbase)
-        : "memory");
-}
 
 // pmc_lj4_signed_m with the r2 floor as ONE v_max_f32 (|r2s| is a free source modifier; the
 // compiler's fmaxf would add canonicalizing maxes, the C form a compare + select): identical
@@ -481,8 +446,6 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
     float* py_ = px_ + stride;
     float* pz_ = py_ + stride;
     float* buf = pz_ + stride;                  // term list: signed r2 values
-    [[maybe_unused]] const uint32_t buf_off = (uint32_t)wave_uniform((int)(uint32_t)(uintptr_t)(
-        const __attribute__((address_space(3))) char*)buf);   // LDS byte address (PMC_CMPX)
     const int ta = cg.ta, tb = cg.tb, x = cg.x, y = cg.y, zg0 = cg.zg0;
     const uint32_t c = cg.c, id = cg.id;
     const bool edge = cg.edge;
@@ -498,7 +461,6 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
     const int n_own = __builtin_amdgcn_readlane(k_cnt, hb);    // lane hb = own cell
     if (n_own == 0) return true;                                // subsweep.h:252-253
     PMC_STAMP(4);
-    const int cap_nb = cap - n_own;
     // slot i's Fisher-Yates index sits on lane jb + i (the prologue's layout: the cell's half)
     int jb = hb;
     if (n_own > fy_have) {                         // rare: slots beyond the prologue's, on lane i
@@ -535,10 +497,24 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
     }
 
     PMC_STAMP(5);
-    // ---- 3. stage neighbours (filtered, compacted) then the own cell -------------------------
+    // ---- 3. stage the own cell (shuffled) into slots [0, n_own), then the neighbours --------
+    // (filtered, compacted) after it (spec v11; v10 staged the own cell after the neighbours).
+    // Own slot i holds particle i of the shuffled order, so a moving particle's slot is always
+    // in the first 64-partner block and the moves leave it out of their term lists by one mask
+    // bit (no LDS store to park it at +inf and restore it).
+    {
+        const float sxo = as_f(__shfl(as_i(ownx), perm));
+        const float syo = as_f(__shfl(as_i(owny), perm));
+        const float szo = as_f(__shfl(as_i(ownz), perm));
+        if (lane < n_own) {
+            px_[lane] = sxo + 0.0f;
+            py_[lane] = syo + 0.0f;
+            pz_[lane] = szo + 0.0f;
+        }
+    }
     float blo[3], bhi[3];
     pmc_cell_box(x, y, zg0, g.w, g.Lx, g.Ly, g.Lz, blo, bhi);
-    int S_nb = 0;
+    int S_nb = n_own;   // next free slot
     // interior waves skip the image adds (an add of +0 changes nothing downstream -- staged
     // coordinates only enter differences that are squared)
     // append the lanes of `valid` whose partner passes the box filter, in lane order
@@ -546,7 +522,7 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
         const unsigned long long mk = __builtin_amdgcn_ballot_w64(pmc_box_d2(ux, uy, uz, blo, bhi) <= g.rc2f) & valid;
         const int nk = wave_uniform(__popcll(mk));
         // otherwise the cell goes to the fallback; exec-masked stores of the kept lanes
-        if (S_nb + nk <= cap_nb && __builtin_amdgcn_inverse_ballot_w64(mk)) {
+        if (S_nb + nk <= cap && __builtin_amdgcn_inverse_ballot_w64(mk)) {
             float* dst = px_ + S_nb + mbcnt64(mk);
             dst[0] = ux;
             dst[stride] = uy;
@@ -601,18 +577,8 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
     else stage(std::false_type{});
     PMC_STAMP(6);
     S_nb = wave_uniform(S_nb);   // keep it scalar past the divergent stores (structurizer joins)
-    if (S_nb > cap_nb) return false;                            // -> full-capacity fallback
-    {
-        const float sxo = as_f(__shfl(as_i(ownx), perm));
-        const float syo = as_f(__shfl(as_i(owny), perm));
-        const float szo = as_f(__shfl(as_i(ownz), perm));
-        if (lane < n_own) {
-            px_[S_nb + lane] = sxo + 0.0f;
-            py_[S_nb + lane] = syo + 0.0f;
-            pz_[S_nb + lane] = szo + 0.0f;
-        }
-    }
-    const int K = S_nb + n_own;
+    if (S_nb > cap) return false;                               // -> full-capacity fallback
+    const int K = S_nb;
     // slots [K, roundup64(K)) are read by the last 64-lane block of every move: make them "far"
     // (+inf -> r2 = inf, never listed).  roundup64(K) <= stride; the clamp keeps every lane's
     // store inside the x row.
@@ -663,7 +629,7 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
                 float* slot = mvs + 2 * (r0 + jl);
                 const float2 mva = *(const float2*)slot;            // (d0, d1)
                 const float d2 = slot[stride];                      // d2 (z tail)
-                const int sp = S_nb + pj;
+                const int sp = pj;                                  // own slot = particle
                 const float qx = px_[sp] + mva.x;                   // make_move: x + g * sigma
                 const float qy = py_[sp] + mva.y;
                 const float qz = pz_[sp] + d2;
@@ -685,10 +651,11 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
                 const float2 qa = *(const float2*)slot;             // (qx, qy)
                 const float2 qb = *(const float2*)(slot + stride);  // (qz, T)
                 const float qx = qa.x, qy = qa.y, qz = qb.x, Fm = qb.y;   // Fm: T's acceptance bound
-                const int si = __builtin_amdgcn_readlane(sp_l, j);  // S_nb + particle of move j
+                const int si = __builtin_amdgcn_readlane(sp_l, j);  // slot = particle of move j (< 64)
                 const float xi = px_[si], yi = py_[si], zi = pz_[si];
                 ++n_ev;
-                px_[si] = kFar;          // exclude the moving particle from its own term list
+                // the moving particle is left out of its own term list: its lane in block 0
+                const unsigned long long sbit = 1ull << si;
                 // 4a. term list: per block of 64 partners, the new-position terms within the
                 // cutoff, then the old-position ones (sign bit set), compacted by ballot+mbcnt.
                 // ~80% of staged pairs lie beyond rc for a given position; they are exactly 0
@@ -696,9 +663,9 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
                 int C = 0;   // wave-uniform
                 // list one block's terms: the new-position ones within the cutoff, then the
                 // old-position ones (negated r2, sign bit set), compacted by ballot + mbcnt
-                auto list = [&](float r2n, float r2on) {
-                    const unsigned long long mn = __builtin_amdgcn_ballot_w64(r2n <= rc2);
-                    const unsigned long long mo = __builtin_amdgcn_ballot_w64(r2on >= nrc2);
+                auto list = [&](float r2n, float r2on, unsigned long long excl) {
+                    const unsigned long long mn = __builtin_amdgcn_ballot_w64(r2n <= rc2) & ~excl;
+                    const unsigned long long mo = __builtin_amdgcn_ballot_w64(r2on >= nrc2) & ~excl;
                     const int cn = C + __popcll(mn);
                     // exec-masked stores (2 SALU each) beat a select into a discard slot (one
                     // half-rate v_cndmask per list on gfx950); packed f32 for the distances
@@ -707,25 +674,21 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
                     if (__builtin_amdgcn_inverse_ballot_w64(mo)) buf[mbcnt64_add(mo, cn)] = r2on;
                     C = cn + __popcll(mo);
                 };
-                auto block = [&](int base) {
-                    // slots >= K and the moving slot hold +inf in x: their r2 is inf, never listed
+                auto block = [&](int base, unsigned long long excl) {
+                    // slots >= K hold +inf in x: their r2 is inf, never listed; the moving slot
+                    // (block 0) is cleared from the masks by excl
                     const int k = base + lane;
                     const float xj = px_[k], yj = py_[k], zj = pz_[k];
                     // old-position term computed negated (= -r2o bit for bit, pmc_r2_neg):
                     // listed with its sign bit set at no extra instruction
-#if PMC_CMPX
-                    list_block_cmpx(pmc_r2(qx - xj, qy - yj, qz - zj), pmc_r2_neg(xi - xj, yi - yj, zi - zj),
-                                    rc2, nrc2, buf_off, C);
-#else
-                    list(pmc_r2(qx - xj, qy - yj, qz - zj), pmc_r2_neg(xi - xj, yi - yj, zi - zj));
-#endif
+                    list(pmc_r2(qx - xj, qy - yj, qz - zj), pmc_r2_neg(xi - xj, yi - yj, zi - zj), excl);
                 };
                 if constexpr (NB > 0) {
 #pragma unroll
-                    for (int b = 0; b < NB; ++b) block(b * kWave);
+                    for (int b = 0; b < NB; ++b) block(b * kWave, b == 0 ? sbit : 0ull);
                 } else {
-                    block(0);
-                    for (int base = kWave; base < K; base += kWave) block(base);
+                    block(0, sbit);
+                    for (int base = kWave; base < K; base += kWave) block(base, 0ull);
                 }
                 // 4b. energies of the listed terms: term t on lane t % 64, ascending t.  The 64
                 // slots after the list get kPad (r2 = 1e30: inv^3 underflows to +0, so the term
@@ -760,8 +723,8 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
                 // so dE = 4s equals the oracle's sum of the 4u, bit for bit, in any association
                 const float sq = wave_sum_fixed_order_s(acc);           // SGPR
                 const bool acc_mv = sq <= Fm;                            // accept_move, subsweep.h:209-216
-                px_[si] = acc_mv ? qx : xi;                              // (every lane, same value)
                 if (acc_mv) {
+                    px_[si] = qx;
                     py_[si] = qy;
                     pz_[si] = qz;
                     ++n_acc;
@@ -789,16 +752,16 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
     if (lane < n_own) {
         using A = DiskAddr<OFF32>;
         const uint32_t off = (c * (uint32_t)(3 * nm) + (uint32_t)lane) * A::kUnit;
-        A::st(disk, off, px_[S_nb + lane]);
-        A::st(disk, off + (uint32_t)nm * A::kUnit, py_[S_nb + lane]);
-        A::st(disk, off + 2u * (uint32_t)nm * A::kUnit, pz_[S_nb + lane]);
+        A::st(disk, off, px_[lane]);
+        A::st(disk, off + (uint32_t)nm * A::kUnit, py_[lane]);
+        A::st(disk, off + 2u * (uint32_t)nm * A::kUnit, pz_[lane]);
         if constexpr (MIRROR) {
             const uint32_t r = mirror_mode == 0 ? (uint32_t)ta + (uint32_t)tb * (uint32_t)(g.cps_x >> 1)
                                                 : (uint32_t)x + (uint32_t)g.cps_x * (uint32_t)y;
             float* m = mirror + (size_t)r * (3 * nm) + lane;
-            m[0] = px_[S_nb + lane];
-            m[nm] = py_[S_nb + lane];
-            m[2 * nm] = pz_[S_nb + lane];
+            m[0] = px_[lane];
+            m[nm] = py_[lane];
+            m[2 * nm] = pz_[lane];
         }
     }
     // fixed-point conversion only when something was accepted (pmc_to_fixed(0) == 0)
