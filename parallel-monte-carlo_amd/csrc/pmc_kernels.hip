@@ -1503,6 +1503,15 @@ __device__ __forceinline__ EnergyStencil energy_stencil(const DevGeom& g, const 
     return e;
 }
 
+// fixed-point term of a mutual pair (weight 2), r2 <= rc2 already tested: 2 * pmc_to_fixed((double)
+// pmc_lj_from_r2(r2, rc2)) bit for bit
+__device__ __forceinline__ int64_t energy_term_w2(float r2, float r2min) {
+    const float rr = r2 < r2min ? r2min : r2;
+    const float inv = pmc_recip(rr);
+    const float p6 = inv * inv * inv;
+    return 2 * pmc_to_fixed_f32(4.0f * (p6 * p6 - p6));
+}
+
 // fixed-point term of a listed pair: r2s = +r2 (weight 1) or -r2 (weight 2), r2 <= rc2 already
 // tested; the value is pmc_to_fixed((double)pmc_lj_from_r2(r2, rc2)) bit for bit
 __device__ __forceinline__ int64_t energy_term(float r2s, float r2min) {
@@ -1531,6 +1540,12 @@ __device__ __forceinline__ int64_t energy_term(float r2s, float r2min) {
 #define PMC_ENERGY_CELLS 16
 #endif
 constexpr int kEnergyCells = PMC_ENERGY_CELLS;
+// edge cells per wave (MODE 1): at 128^3 the ~98k edge cells are well under one round of the chip's
+// wave slots at 16 per wave, so the launch lasts one long wave lifetime; shorter waves spread them
+#ifndef PMC_ENERGY_EDGE_CELLS
+#define PMC_ENERGY_EDGE_CELLS 4
+#endif
+constexpr int kEdgeCells = PMC_ENERGY_EDGE_CELLS;
 // own particles per pair-loop step (1 or 2: two broadcast particles share the loop control, the
 // ring accounting and the drain test)
 #ifndef PMC_ENERGY_STEP
@@ -1540,11 +1555,17 @@ constexpr int kEnergyRing = PMC_ENERGY_STEP == 2 ? 256 : 128;
 
 // k_energy_rows: one wave per row segment of kESeg cells along x; the 9 neighbouring rows of the
 // segment (kESeg + 2 cells each) are staged once, kECap particles at most
-constexpr int kESeg = 8;
+// Segment length and staging capacity keep a wave's LDS within 5 KiB (8 waves per SIMD; round 3's
+// 8-cell segments with 384 staged particles took 6.5 KiB: 6 waves per SIMD).  At 128^3/1e7 a
+// 6-cell segment stages 186 particles on average; the near-lattice start peaks at 281.
+#ifndef PMC_ENERGY_SEG
+#define PMC_ENERGY_SEG 6
+#endif
+constexpr int kESeg = PMC_ENERGY_SEG;
 constexpr int kERows = 5;                   // the rows of an interior cell's half shell
 constexpr int kEStaged = kERows * (kESeg + 2);   // staged cells per segment (< 64: one lane each)
 static_assert(kEStaged < 64, "one lane per staged cell");
-constexpr int kECap = 384;                  // staged particles (4.77 per cell: ~240; near-lattice states +4.5 sd)
+constexpr int kECap = kESeg == 6 ? 288 : 384;   // staged particles
 constexpr int kEList = 14 * 16;             // a cell's filtered partner list (indices into the staging)
 
 // A cell is an "edge" cell for the energy when a stencil neighbour is wrapped across the periodic
@@ -1816,8 +1837,8 @@ __global__ __launch_bounds__(kWave) void k_energy(DevGeom g, const float* __rest
         // the rows y = 0 and cps_y-1 and the cells x = 0 and cps_x-1 of the rows between
         const uint32_t P = (uint32_t)g.cps_x * (uint32_t)g.cps_y;
         const uint32_t M = 2u * (uint32_t)g.cps_x + 2u * (uint32_t)(g.cps_y - 2);
-        const uint32_t k0 = blockIdx.x * (uint32_t)kEnergyCells;
-        const int ncl = (int)(total_cells - k0 < (uint32_t)kEnergyCells ? total_cells - k0 : (uint32_t)kEnergyCells);
+        const uint32_t k0 = blockIdx.x * (uint32_t)kEdgeCells;
+        const int ncl = (int)(total_cells - k0 < (uint32_t)kEdgeCells ? total_cells - k0 : (uint32_t)kEdgeCells);
         uint32_t k = k0;
         run_cells(ncl, [&]() -> uint32_t {
             const uint32_t kk = k++;
@@ -1877,7 +1898,7 @@ __global__ __launch_bounds__(kWave) void k_energy_rows(DevGeom g, const float* _
     float* ey_ = rsm + kECap;
     float* ez_ = rsm + 2 * kECap;
     float* ring = rsm + 3 * kECap;                    // listed pairs (signed r2), kEnergyRing
-    int* lst = (int*)(ring + kEnergyRing);            // the own cell's partners (staged indices)
+    uint16_t* lst = (uint16_t*)(ring + kEnergyRing);  // the own cell's partners (staged indices)
     int2* rec = (int2*)(lst + kEList);                // staged cell: storage index, start | count << 16
     const int lane = threadIdx.x;
     const int nm = g.nmax;
@@ -1980,7 +2001,7 @@ __global__ __launch_bounds__(kWave) void k_energy_rows(DevGeom g, const float* _
         // within the cutoff of the own cell's (padded) box
         float blo[3], bhi[3];
         pmc_cell_box(x, y, zg, g.w, g.Lx, g.Ly, g.Lz, blo, bhi);
-        if (lane < n_own) lst[lane] = sA + lane;
+        if (lane < n_own) lst[lane] = (uint16_t)(sA + lane);
         int S = n_own;
         for (int jb = 0; jb < T; jb += kWave) {
             const int j = jb + lane;
@@ -1989,7 +2010,7 @@ __global__ __launch_bounds__(kWave) void k_energy_rows(DevGeom g, const float* _
             const int sj = j < T ? src : 0;
             const bool keep = j >= n_own && j < T && pmc_box_d2(ex_[sj], ey_[sj], ez_[sj], blo, bhi) <= g.rc2f;
             const unsigned long long mk = __builtin_amdgcn_ballot_w64(keep);
-            if (keep) lst[S + mbcnt64(mk)] = sj;
+            if (keep) lst[S + mbcnt64(mk)] = (uint16_t)sj;
             S += __popcll(mk);
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1998,28 +2019,36 @@ __global__ __launch_bounds__(kWave) void k_energy_rows(DevGeom g, const float* _
         const float oz = lane < n_own ? ez_[sA + lane] : 0.0f;
         int head = 0, C = 0;
         auto drain = [&](int lim) {
-            if (lane < lim) sum += energy_term(ring[(head + lane) & RM], r2min);
+            if (lane < lim) sum += energy_term_w2(ring[(head + lane) & RM], r2min);
             head = (head + 64) & RM;
             C -= lim;
         };
-        for (int jb = 0; jb < S; jb += kWave) {
+        // one 64-partner block against every own particle i (broadcast by v_readlane); in block 0
+        // the own slots j <= i are left out by a running mask (bit i cleared per step): the pairs
+        // j > i of the own cell.  Every listed pair is mutual (weight 2: no sign bit).
+        auto pairs = [&](int jb, auto first) {
             const int j = jb + lane;
             const int sj = lst[j < S ? j : 0];
             const float xj = ex_[sj], yj = ey_[sj], zj = ez_[sj];
             unsigned long long vm = __builtin_amdgcn_ballot_w64(j < S);
+            unsigned long long bit = 1ull;                // own slot i (block 0)
             for (int i = 0; i < n_own; ++i) {
                 const float xi = as_f(__builtin_amdgcn_readlane(as_i(ox), i));
                 const float yi = as_f(__builtin_amdgcn_readlane(as_i(oy), i));
                 const float zi = as_f(__builtin_amdgcn_readlane(as_i(oz), i));
                 const float r2 = pmc_r2(xi - xj, yi - yj, zi - zj);
-                if (jb == 0) vm &= vm - 1ull;             // own slots j <= i: lanes 0..i of block 0
+                if constexpr (decltype(first)::value) {
+                    vm &= ~bit;
+                    bit <<= 1;
+                }
                 const unsigned long long im = __builtin_amdgcn_ballot_w64(r2 <= rc2) & vm;
-                if (__builtin_amdgcn_inverse_ballot_w64(im))
-                    ring[(head + C + mbcnt64(im)) & RM] = as_f(as_i(r2) | (int)0x80000000);   // weight 2
+                if (__builtin_amdgcn_inverse_ballot_w64(im)) ring[(head + C + mbcnt64(im)) & RM] = r2;
                 C += __popcll(im);
                 if (C >= 64) drain(64);
             }
-        }
+        };
+        pairs(0, std::true_type{});
+        for (int jb = kWave; jb < S; jb += kWave) pairs(jb, std::false_type{});
         if (C > 0) drain(C);
     }
 #pragma unroll
@@ -2350,7 +2379,9 @@ hipError_t launch_energy(const DevGeom& g, const float* disk, const int16_t* n,
     // (every plane's first and last plane coincide with the slab's halo-neighbour or box-face planes)
     const int64_t n_edge = 2 * (int64_t)g.cps_x * g.cps_y +
                            (int64_t)(g.nz_local - 2) * (2 * (int64_t)g.cps_x + 2 * (int64_t)(g.cps_y - 2));
-    const size_t lds_rows = sizeof(float) * (3 * kECap + kEnergyRing) + sizeof(int) * kEList + sizeof(int2) * 64;
+    const size_t lds_rows = sizeof(float) * (3 * kECap + kEnergyRing) + sizeof(uint16_t) * kEList + sizeof(int2) * 64;
+    static_assert(sizeof(float) * (3 * kECap + kEnergyRing) + sizeof(uint16_t) * kEList + sizeof(int2) * 64 <= 5120 || kESeg != 6,
+                  "energy rows: 8 waves per SIMD");
     const dim3 grid_rows((unsigned)energy_segments(g));
     auto go = [&](auto k0, auto k1, auto k2, auto kr) {
         if (legacy) {
@@ -2358,7 +2389,7 @@ hipError_t launch_energy(const DevGeom& g, const float* disk, const int16_t* n,
             return;
         }
         hipLaunchKernelGGL(kr, grid_rows, block, lds_rows, st, g, disk, n, acc, segq, div_nsx, div_cy, cap);
-        hipLaunchKernelGGL(k1, dim3((unsigned)((n_edge + kEnergyCells - 1) / kEnergyCells)), block, lds, st, g, disk, n,
+        hipLaunchKernelGGL(k1, dim3((unsigned)((n_edge + kEdgeCells - 1) / kEdgeCells)), block, lds, st, g, disk, n,
                            acc, (uint32_t)n_edge, segq, div_nsx);
         hipLaunchKernelGGL(k2, dim3(64), block, lds, st, g, disk, n, acc, tc, segq, div_nsx);
     };
