@@ -628,8 +628,8 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
                 const int pj = (i + jl) >= n_own ? i + jl - n_own : i + jl;
                 float* slot = mvs + 2 * (r0 + jl);
                 const float2 mva = *(const float2*)slot;            // (d0, d1)
-                const float d2 = slot[stride];                      // d2 (z tail)
                 const int sp = pj;                                  // own slot = particle
+                const float d2 = slot[stride];                      // d2 (z tail)
                 const float qx = px_[sp] + mva.x;                   // make_move: x + g * sigma
                 const float qy = py_[sp] + mva.y;
                 const float qz = pz_[sp] + d2;
@@ -646,12 +646,12 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
             }
             while (pend) {
                 const int j = (int)__builtin_ctzll(pend);
-                pend &= pend - 1ull;
+                asm volatile("s_bitset0_b64 %0, %1" : "+s"(pend) : "s"(j));   // pend &= ~(1 << j)
+                const int si = __builtin_amdgcn_readlane(sp_l, j);  // slot = particle of move j (< 64)
                 const float* slot = mvs + 2 * (r0 + j);
                 const float2 qa = *(const float2*)slot;             // (qx, qy)
                 const float2 qb = *(const float2*)(slot + stride);  // (qz, T)
                 const float qx = qa.x, qy = qa.y, qz = qb.x, Fm = qb.y;   // Fm: T's acceptance bound
-                const int si = __builtin_amdgcn_readlane(sp_l, j);  // slot = particle of move j (< 64)
                 const float xi = px_[si], yi = py_[si], zi = pz_[si];
                 ++n_ev;
                 // the moving particle is left out of its own term list: its lane in block 0
@@ -1014,6 +1014,10 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_fallback(DevGeom
     const int full = 27 * (NMC > 0 ? NMC : g.nmax);
     float* px_ = smem + wv * lds_floats_per_wave(full);
     const int count = __builtin_amdgcn_readfirstlane(ovf[kOvfCount]);
+    // nothing queued (the common case): nothing to clear either -- every workgroup reads the same
+    // count, so either all of them take part in the done-counting below or none does (no atomic
+    // round trip on the phase's critical path)
+    if (count == 0) return;
     for (int e = (int)blockIdx.x * kSubWaves + wv; e < count; e += (int)gridDim.x * kSubWaves) {
         const int t = __builtin_amdgcn_readfirstlane(ovf[kOvfHead + e]);
         (void)subsweep_wave<NSLOT, NMC, 27 * NMC, OFF32, MIRROR>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, full,
@@ -1567,6 +1571,9 @@ constexpr int kEStaged = kERows * (kESeg + 2);   // staged cells per segment (< 
 static_assert(kEStaged < 64, "one lane per staged cell");
 constexpr int kECap = kESeg == 6 ? 288 : 384;   // staged particles
 constexpr int kEList = 14 * 16;             // a cell's filtered partner list (indices into the staging)
+#ifndef PMC_ENERGY_OWN_LDS
+#define PMC_ENERGY_OWN_LDS 1   // pair loop: own particle from LDS (1) or by v_readlane (0)
+#endif
 
 // A cell is an "edge" cell for the energy when a stencil neighbour is wrapped across the periodic
 // box or lies in a halo plane (slab mode): its pairs with that neighbour are directed (weight 1,
@@ -2033,9 +2040,15 @@ __global__ __launch_bounds__(kWave) void k_energy_rows(DevGeom g, const float* _
             unsigned long long vm = __builtin_amdgcn_ballot_w64(j < S);
             unsigned long long bit = 1ull;                // own slot i (block 0)
             for (int i = 0; i < n_own; ++i) {
+#if PMC_ENERGY_OWN_LDS
+                // own particle i broadcast from the staging (uniform address: one LDS read per
+                // coordinate) instead of three v_readlane
+                const float xi = ex_[sA + i], yi = ey_[sA + i], zi = ez_[sA + i];
+#else
                 const float xi = as_f(__builtin_amdgcn_readlane(as_i(ox), i));
                 const float yi = as_f(__builtin_amdgcn_readlane(as_i(oy), i));
                 const float zi = as_f(__builtin_amdgcn_readlane(as_i(oz), i));
+#endif
                 const float r2 = pmc_r2(xi - xj, yi - yj, zi - zj);
                 if constexpr (decltype(first)::value) {
                     vm &= ~bit;
