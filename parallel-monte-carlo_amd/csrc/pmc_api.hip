@@ -611,16 +611,18 @@ int pmc_run_small(pmc_ctx* c, uint32_t first, int count) {
     return PMC_OK;
 }
 
-// pmc_start runs the boxes where one launch on XCD 0 beats 17 launches over the 8 XCDs through
-// pmc_run_small: at most 64 cells per colour (8^3: 0.115 against 0.124 ms per sweep; at 16^3 one
-// XCD is 4x slower than the whole chip, profiles/r03n_small_box.txt).  PMC_SMALL=0: never.
+// pmc_start runs every box with eager launches: since small colour phases run as one full-capacity
+// launch each (k_subsweep_full, 9 launches per sweep), they beat pmc_run_small's single launch on
+// XCD 0 at every size (8^3: 0.070 against 0.110 ms per sweep, 16^3: 0.072 against 0.70 ms,
+// profiles/r03sm_small_box.txt; round 3 had picked pmc_run_small for <= 64 cells per colour against
+// the 17-launch sweep).  PMC_SMALL=1 restores that choice; pmc_run_small stays callable.
 static bool use_small(const pmc_ctx* c) {
-    static const bool off = [] {
+    static const bool on = [] {
         const char* v = std::getenv("PMC_SMALL");
-        return v && std::atoi(v) == 0;
+        return v && std::atoi(v) == 1;
     }();
     const int64_t per_colour = (int64_t)(c->P.cps_x / 2) * (c->P.cps_y / 2) * (c->P.cps_z / 2);
-    return !off && small_sweep_participants(c->G) > 0 && per_colour <= 64;
+    return on && small_sweep_participants(c->G) > 0 && per_colour <= 64;
 }
 
 int pmc_start_ex(pmc_ctx* c, uint32_t first, int mc_passes, int flags, pmc_result* out) {

@@ -1040,6 +1040,37 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_fallback(DevGeom
     }
 }
 
+// Small launches (a colour phase of at most PMC_SMALL_LAUNCH cells, default 8192: boxes up to
+// ~40^3): one cell per wave at full capacity (27*nmax partners, nothing overflows), so the phase is
+// ONE launch -- no fallback launch after it -- and its waves live half as long as the main launch's
+// two-cell waves.  Below a round of the chip's wave slots a phase lasts about one wave lifetime plus
+// the launch, so both halve.  Same per-cell code as every other path: results bit-identical.
+template <int NSLOT, int NMC, bool OFF32>
+__global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_full(DevGeom g, float* __restrict__ disk,
+                                                                       const int16_t* __restrict__ ncnt,
+                                                                       int ox, int oy, int oz, uint32_t sweep,
+                                                                       unsigned long long* __restrict__ stats,
+                                                                       int cz0, int ncz) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int full = 27 * (NMC > 0 ? NMC : g.nmax);
+    float* px_ = smem + wv * lds_floats_per_wave(full);
+    const int total = (g.cps_x >> 1) * (g.cps_y >> 1) * ncz;
+    const int t = (int)blockIdx.x * kSubWaves + wv;
+    if (t >= total) return;
+    (void)subsweep_wave<NSLOT, NMC, 27 * NMC, OFF32>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, full, full, t, cz0);
+}
+
+// colour phases of at most this many cells use k_subsweep_full (PMC_SMALL_LAUNCH; 0 disables it).
+// Measured (profiles/r03sl_small_launch.txt): 16^3 0.122 -> 0.073 ms per sweep, 24^3 0.141 ->
+// 0.087, 32^3 0.144 -> 0.098; larger launches are faster with the main kernel (48^3: 0.209 against
+// 0.225, 64^3: 0.396 against 0.505), and so are the slab's boundary-plane launches, which share the
+// chip with the interior chains (4-rank rehearsal 0.682 against 0.692 ms per rank sweep).
+static int64_t env_cells(const char* name, int64_t dflt) {
+    const char* v = std::getenv(name);
+    return v ? (int64_t)std::atoll(v) : dflt;
+}
+
 // ------------------------------------------------------------------------------------------
 // Small boxes: whole sweeps in ONE launch on ONE XCD (pmc_run_small).
 //
@@ -2021,9 +2052,11 @@ __global__ __launch_bounds__(kWave) void k_energy_rows(DevGeom g, const float* _
             S += __popcll(mk);
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#if !PMC_ENERGY_OWN_LDS
         const float ox = lane < n_own ? ex_[sA + lane] : 0.0f;
         const float oy = lane < n_own ? ey_[sA + lane] : 0.0f;
         const float oz = lane < n_own ? ez_[sA + lane] : 0.0f;
+#endif
         int head = 0, C = 0;
         auto drain = [&](int lim) {
             if (lane < lim) sum += energy_term_w2(ring[(head + lane) & RM], r2min);
@@ -2161,6 +2194,13 @@ static void launch_subsweep_t(const DevGeom& g, float* disk, const int16_t* n, i
     const int64_t blocks = (waves + kSubWaves - 1) / kSubWaves;
     const int cap = subsweep_capacity(g);
     const int full = 27 * g.nmax;
+    static const int64_t small_cells = env_cells("PMC_SMALL_LAUNCH", 8192);
+    if (total <= small_cells) {   // one launch, one full-capacity cell per wave (k_subsweep_full)
+        const size_t lds_full = sizeof(float) * (size_t)lds_floats_per_wave(full) * kSubWaves;
+        launch_k(k_subsweep_full<NSLOT, NMC, OFF32>, dim3((unsigned)((total + kSubWaves - 1) / kSubWaves)),
+                 dim3(kWave * kSubWaves), lds_full, st, tm, g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz);
+        return;
+    }
     size_t lds = sizeof(float) * (size_t)lds_floats_per_wave(kMainCap) * kSubWaves;
 #ifdef PMC_PROBE_LDS_MULT   // timing probe only: fewer waves per SIMD through a larger LDS request
     lds = lds * PMC_PROBE_LDS_MULT / 100;

@@ -319,14 +319,17 @@ def test_single_colour_parity_128(pmc, oracle):
     assert abs(r["e_initial"] + r["de_fixed"] / 2**32 - r["e_final"]) < 1e-4 * abs(r["e_final"])
 
 
-@pytest.mark.parametrize("env,nmax", [({"PMC_SUBSWEEP_CAP": "64"}, 32),
+@pytest.mark.parametrize("env,nmax", [({"PMC_SUBSWEEP_CAP": "64", "PMC_SMALL_LAUNCH": "0"}, 32),
                                       ({"PMC_FORCE_ADDR64": "1"}, 16),
-                                      ({"PMC_FORCE_ADDR64": "1", "PMC_SUBSWEEP_CAP": "64"}, 16)])
+                                      ({"PMC_FORCE_ADDR64": "1", "PMC_SUBSWEEP_CAP": "64", "PMC_SMALL_LAUNCH": "0"}, 16),
+                                      ({"PMC_SMALL_LAUNCH": "0"}, 16)])
 def test_fallback_and_addr64_paths(oracle, env, nmax):
     """Test hooks for launch variants the default configs never take, each bit-identical to the
     oracle: PMC_SUBSWEEP_CAP forces a tiny LDS capacity, so (almost) every cell goes to the
     full-capacity fallback launch; PMC_FORCE_ADDR64 forces the 64-bit disk addressing used for
-    buffers of 4 GiB and more.  Runs in a subprocess (the hooks are read once)."""
+    buffers of 4 GiB and more; PMC_SMALL_LAUNCH=0 takes this 8^3 box through the main two-cell
+    launch + fallback instead of the one-launch full-capacity path small boxes default to.  Runs in
+    a subprocess (the hooks are read once)."""
     import os
     import subprocess
     import sys
@@ -428,7 +431,7 @@ print("ok", drv.ctx.stats())
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = subprocess.run([sys.executable, "-c", code, os.path.join(repo, "parallel-monte-carlo_amd"),
                           os.path.join(repo, "oracle"), "1" if rccl else "0"],
-                         env=dict(os.environ, PMC_SUBSWEEP_CAP="64"), capture_output=True, text=True, timeout=300)
+                         env=dict(os.environ, PMC_SUBSWEEP_CAP="64", PMC_SMALL_LAUNCH="0"), capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-2000:]
     assert any(line.startswith("ok") for line in out.stdout.splitlines()), out.stdout[-2000:]   # (RCCL may print too)
 
