@@ -3,7 +3,7 @@
   PMC_LIB_PATH=.../lib_stamps.so python tools/stamps.py
 
 Stamps per cell visit (main launch): 0 entry, 1 stencil table + count load issued, 2 row loads
-issued, 3 RNG done, 4 own count known, 5 shuffle done, 6 neighbours staged, 7 own cell staged,
+issued, 3 RNG done, 4 own count known, 5 shuffle done, 6 own cell + neighbours staged (v11), 7 far pad,
 8 moves done, 9 written back.
 """
 import ctypes as C
@@ -29,7 +29,7 @@ L = pmc_amd._lib.lib()
 L.pmc_debug_stamps.restype = C.c_int
 L.pmc_debug_stamps.argtypes = [C.c_size_t, C.c_void_p]
 ncell = (cps // 2) ** 3
-names = ["stencil+cnt", "row loads", "rng", "count wait", "shuffle", "staging", "own stage", "moves", "writeback"]
+names = ["stencil+cnt", "row loads", "rng", "count wait", "shuffle", "own+nb staging", "far pad", "moves", "writeback"]   # spec v11: own cell staged first
 for rep in range(2):
     assert L.pmc_debug_stamps(ncell, None) == 0
     t0 = time.perf_counter()
