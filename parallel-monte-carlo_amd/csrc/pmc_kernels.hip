@@ -458,6 +458,10 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
     const float ownx = ld.ownx, owny = ld.owny, ownz = ld.ownz;
     // single-cell RNG chunk: moves m0..m0+15 (lanes 0-15 MOVE, 16-31 ACCEPT, 32-47 pair B), parked
     auto rng_single = [&](int m0) { rng_chunk_single(g, id, sweep, m0, py_, pz_, lcap4); };
+#ifndef PMC_VISIT_PRIO
+#define PMC_VISIT_PRIO 1   // wave priority of the shuffle, staging and write-back (see PMC_MOVE_PRIO)
+#endif
+    if (PMC_VISIT_PRIO) __builtin_amdgcn_s_setprio(PMC_VISIT_PRIO);
     const int n_own = __builtin_amdgcn_readlane(k_cnt, hb);    // lane hb = own cell
     if (n_own == 0) return true;                                // subsweep.h:252-253
     PMC_STAMP(4);
@@ -737,6 +741,16 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
         }
     }
     };
+#ifndef PMC_MOVE_PRIO
+#define PMC_MOVE_PRIO 2
+#endif
+    // Wave priority by section (s_setprio): the moves at 2, the rest of the visit (shuffle, staging,
+    // write-back) at 1, the prologue (stencil table, loads, RNG) at 0.  The moves' serial chains
+    // (term list -> energy pass -> DPP reduction -> accept) then win VALU arbitration over waves
+    // that are staging, and both over waves whose RNG pass overlaps their loads (same-box A/B,
+    // profiles/r03pr_priority_ab.txt: sweep -0.5%; moves at 1 alone -0.3%; staging above the moves
+    // +1.2%)
+    if (PMC_MOVE_PRIO) __builtin_amdgcn_s_setprio(PMC_MOVE_PRIO);
     if constexpr (LCAP == kMainCap) {
         const int nb = (K + kWave - 1) / kWave;                 // 1..4 (K <= cap <= 224)
         if (nb <= 1) move_loop(std::integral_constant<int, 1>{});
@@ -747,6 +761,7 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
         move_loop(std::integral_constant<int, 0>{});
     }
 
+    if (PMC_MOVE_PRIO) __builtin_amdgcn_s_setprio(PMC_VISIT_PRIO);
     PMC_STAMP(8);
     // ---- 5. write back the own cell in shuffled order (cpy_D_sh_to_Disk, subsweep.h:29-36) ----
     if (lane < n_own) {
