@@ -31,6 +31,12 @@ namespace pmc {
 #ifndef PMC_SHIFT_XCD
 #define PMC_SHIFT_XCD 0   // shiftCells blocks in XCD-contiguous order (A/B)
 #endif
+#ifndef PMC_MOVE_PRIO
+#define PMC_MOVE_PRIO 2    // wave priority of the moves (their serial tail one above); 0: no s_setprio
+#endif
+#ifndef PMC_VISIT_PRIO
+#define PMC_VISIT_PRIO 1   // wave priority of the shuffle, staging and write-back (see visit_cell)
+#endif
 #ifndef PMC_BITOP3
 #define PMC_BITOP3 1   // Philox key/word xors as one v_bitop3_b32 (sweep -0.3%, profiles/r03h_ab.txt)
 #endif
@@ -458,9 +464,6 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
     const float ownx = ld.ownx, owny = ld.owny, ownz = ld.ownz;
     // single-cell RNG chunk: moves m0..m0+15 (lanes 0-15 MOVE, 16-31 ACCEPT, 32-47 pair B), parked
     auto rng_single = [&](int m0) { rng_chunk_single(g, id, sweep, m0, py_, pz_, lcap4); };
-#ifndef PMC_VISIT_PRIO
-#define PMC_VISIT_PRIO 1   // wave priority of the shuffle, staging and write-back (see PMC_MOVE_PRIO)
-#endif
     if (PMC_VISIT_PRIO) __builtin_amdgcn_s_setprio(PMC_VISIT_PRIO);
     const int n_own = __builtin_amdgcn_readlane(k_cnt, hb);    // lane hb = own cell
     if (n_own == 0) return true;                                // subsweep.h:252-253
@@ -717,6 +720,9 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
                     asm volatile("" :: "v"(pv), "s"(ps));
                 }
 #endif
+                // the serial tail (energy pass, reduction, accept) one priority level above
+                // the rest of the moves (same-box A/B: phase -0.5%, profiles/r03pr_priority_ab.txt)
+                if (PMC_MOVE_PRIO) __builtin_amdgcn_s_setprio(PMC_MOVE_PRIO + 1);
                 buf[C + lane] = kPad;
                 // the first pass unconditionally (C == 0 reads only kPad: +0), the rest looped.  (A
                 // lane sum may start at -0 where the oracle's starts 0 + -0 = +0: zeros of either
@@ -727,6 +733,7 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
                 // so dE = 4s equals the oracle's sum of the 4u, bit for bit, in any association
                 const float sq = wave_sum_fixed_order_s(acc);           // SGPR
                 const bool acc_mv = sq <= Fm;                            // accept_move, subsweep.h:209-216
+                if (PMC_MOVE_PRIO) __builtin_amdgcn_s_setprio(PMC_MOVE_PRIO);
                 if (acc_mv) {
                     px_[si] = qx;
                     py_[si] = qy;
@@ -741,9 +748,6 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
         }
     }
     };
-#ifndef PMC_MOVE_PRIO
-#define PMC_MOVE_PRIO 2
-#endif
     // Wave priority by section (s_setprio): the moves at 2, the rest of the visit (shuffle, staging,
     // write-back) at 1, the prologue (stencil table, loads, RNG) at 0.  The moves' serial chains
     // (term list -> energy pass -> DPP reduction -> accept) then win VALU arbitration over waves
@@ -2108,8 +2112,11 @@ __global__ __launch_bounds__(kWave) void k_energy_rows(DevGeom g, const float* _
                 if (C >= 64) drain(64);
             }
         };
+        // the pair loop above the staging of other waves (A/B: -0.7%, profiles/r03pr_priority_ab.txt)
+        __builtin_amdgcn_s_setprio(1);
         pairs(0, std::true_type{});
         for (int jb = kWave; jb < S; jb += kWave) pairs(jb, std::false_type{});
+        __builtin_amdgcn_s_setprio(0);
         if (C > 0) drain(C);
     }
 #pragma unroll
