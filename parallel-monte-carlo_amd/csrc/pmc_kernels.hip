@@ -37,6 +37,9 @@ namespace pmc {
 #ifndef PMC_VISIT_PRIO
 #define PMC_VISIT_PRIO 1   // wave priority of the shuffle, staging and write-back (see visit_cell)
 #endif
+#ifndef PMC_BOUNDARY_PB
+#define PMC_BOUNDARY_PB 1   // slab boundary-plane launches: wave priority one level up (rank sweep -0.6% at 8 ranks, -1.2% at 4)
+#endif
 #ifndef PMC_BITOP3
 #define PMC_BITOP3 1   // Philox key/word xors as one v_bitop3_b32 (sweep -0.3%, profiles/r03h_ab.txt)
 #endif
@@ -434,7 +437,7 @@ __device__ __forceinline__ int fy_words_single(const DevGeom& g, uint32_t id, ui
 // MIRROR (slab boundary planes): the written-back rows also go to `mirror` -- mirror_mode 0: the
 // packed colour buffer of the halo exchange (row ta + tb*cps_x/2), 1: a plane (row x + cps_x*y;
 // the periodic single-rank halo).  Empty cells write nothing (their count stays 0).
-template <int NSLOT, int NMC, int LCAP, bool OFF32, bool MIRROR>
+template <int NSLOT, int NMC, int LCAP, bool OFF32, bool MIRROR, int PB = 0>
 __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__ disk, uint32_t sweep,
                                            unsigned long long* __restrict__ stats, float* __restrict__ px_,
                                            int lcap_rt, int cap, int t, const CellGeo& cg, int hb, int k_cnt,
@@ -464,7 +467,11 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
     const float ownx = ld.ownx, owny = ld.owny, ownz = ld.ownz;
     // single-cell RNG chunk: moves m0..m0+15 (lanes 0-15 MOVE, 16-31 ACCEPT, 32-47 pair B), parked
     auto rng_single = [&](int m0) { rng_chunk_single(g, id, sweep, m0, py_, pz_, lcap4); };
-    if (PMC_VISIT_PRIO) __builtin_amdgcn_s_setprio(PMC_VISIT_PRIO);
+    // (PB: the slab boundary launches run one level higher: the halo exchange waits for them)
+    constexpr int kVisitPrio = PMC_VISIT_PRIO + PB > 3 ? 3 : PMC_VISIT_PRIO + PB;
+    constexpr int kMovePrio = PMC_MOVE_PRIO == 0 ? 0 : (PMC_MOVE_PRIO + PB > 3 ? 3 : PMC_MOVE_PRIO + PB);
+    constexpr int kTailPrio = PMC_MOVE_PRIO == 0 ? 0 : (PMC_MOVE_PRIO + 1 + PB > 3 ? 3 : PMC_MOVE_PRIO + 1 + PB);
+    if (kVisitPrio) __builtin_amdgcn_s_setprio(kVisitPrio);
     const int n_own = __builtin_amdgcn_readlane(k_cnt, hb);    // lane hb = own cell
     if (n_own == 0) return true;                                // subsweep.h:252-253
     PMC_STAMP(4);
@@ -722,7 +729,7 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
 #endif
                 // the serial tail (energy pass, reduction, accept) one priority level above
                 // the rest of the moves (same-box A/B: phase -0.5%, profiles/r03pr_priority_ab.txt)
-                if (PMC_MOVE_PRIO) __builtin_amdgcn_s_setprio(PMC_MOVE_PRIO + 1);
+                if (kTailPrio) __builtin_amdgcn_s_setprio(kTailPrio);
                 buf[C + lane] = kPad;
                 // the first pass unconditionally (C == 0 reads only kPad: +0), the rest looped.  (A
                 // lane sum may start at -0 where the oracle's starts 0 + -0 = +0: zeros of either
@@ -733,7 +740,7 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
                 // so dE = 4s equals the oracle's sum of the 4u, bit for bit, in any association
                 const float sq = wave_sum_fixed_order_s(acc);           // SGPR
                 const bool acc_mv = sq <= Fm;                            // accept_move, subsweep.h:209-216
-                if (PMC_MOVE_PRIO) __builtin_amdgcn_s_setprio(PMC_MOVE_PRIO);
+                if (kMovePrio) __builtin_amdgcn_s_setprio(kMovePrio);
                 if (acc_mv) {
                     px_[si] = qx;
                     py_[si] = qy;
@@ -754,7 +761,7 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
     // that are staging, and both over waves whose RNG pass overlaps their loads (same-box A/B,
     // profiles/r03pr_priority_ab.txt: sweep -0.5%; moves at 1 alone -0.3%; staging above the moves
     // +1.2%)
-    if (PMC_MOVE_PRIO) __builtin_amdgcn_s_setprio(PMC_MOVE_PRIO);
+    if (kMovePrio) __builtin_amdgcn_s_setprio(kMovePrio);
     if constexpr (LCAP == kMainCap) {
         const int nb = (K + kWave - 1) / kWave;                 // 1..4 (K <= cap <= 224)
         if (nb <= 1) move_loop(std::integral_constant<int, 1>{});
@@ -765,7 +772,7 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
         move_loop(std::integral_constant<int, 0>{});
     }
 
-    if (PMC_MOVE_PRIO) __builtin_amdgcn_s_setprio(PMC_VISIT_PRIO);
+    if (kMovePrio) __builtin_amdgcn_s_setprio(kVisitPrio);
     PMC_STAMP(8);
     // ---- 5. write back the own cell in shuffled order (cpy_D_sh_to_Disk, subsweep.h:29-36) ----
     if (lane < n_own) {
@@ -812,7 +819,7 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
 
 // The single-cell prologue: stencil table on lanes 0-26, the visit's loads, then one RNG pass
 // (moves 0-15 and FY words of slots 0-63) while the loads fly.
-template <int NSLOT, int NMC, int LCAP, bool OFF32, bool MIRROR = false>
+template <int NSLOT, int NMC, int LCAP, bool OFF32, bool MIRROR = false, int PB = 0>
 __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restrict__ disk,
                                               const int16_t* __restrict__ ncnt, int ox, int oy, int oz,
                                               uint32_t sweep, unsigned long long* __restrict__ stats,
@@ -839,7 +846,8 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     rng_chunk_single(g, cg.id, sweep, 0, py_, pz_, lcap4);
     const int jv = fy_words_single(g, cg.id, sweep, buf);
     PMC_STAMP(3);
-    return visit_cell<NSLOT, NMC, LCAP, OFF32, MIRROR>(g, disk, sweep, stats, px_, lcap_rt, cap, t, cg, 0, k_cnt,
+    if (PB) __builtin_amdgcn_s_setprio(PB);
+    return visit_cell<NSLOT, NMC, LCAP, OFF32, MIRROR, PB>(g, disk, sweep, stats, px_, lcap_rt, cap, t, cg, 0, k_cnt,
                                                        k_off, sl.sx, sl.sy, sl.sz, ld, jv, 64, 16, mirror,
                                                        mirror_mode);
 }
@@ -1010,10 +1018,10 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_direct(DevGeom g
     if (t >= total) return;
     bool ok;
     if (mirror)
-        ok = subsweep_wave<NSLOT, NMC, kMainCap, OFF32, true>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, kMainCap,
+        ok = subsweep_wave<NSLOT, NMC, kMainCap, OFF32, true, PMC_BOUNDARY_PB>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, kMainCap,
                                                              cap, t, cz0, mirror, mirror_mode);
     else
-        ok = subsweep_wave<NSLOT, NMC, kMainCap, OFF32>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, kMainCap, cap,
+        ok = subsweep_wave<NSLOT, NMC, kMainCap, OFF32, false, PMC_BOUNDARY_PB>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, kMainCap, cap,
                                                        t, cz0);
     if (!ok && (threadIdx.x & (kWave - 1)) == 0) ovf[kOvfHead + atomicAdd(&ovf[kOvfCount], 1)] = t;
 }
