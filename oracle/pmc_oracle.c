@@ -472,6 +472,21 @@ int orc_run(const pmc_params* p, float* disk, int16_t* n, float* sdisk, int16_t*
     return over ? PMC_ERR_OVERFLOW : PMC_OK;
 }
 
+/* orc_run with the energy trace of kernel.cu:643,695 (calc_energy after every sweep there): the
+ * cell-list energy after every `every`-th sweep into trace[nsweeps / every] -- one C call for the
+ * statistical tests' long chains */
+int orc_run_trace(const pmc_params* p, float* disk, int16_t* n, float* sdisk, int16_t* sn,
+                  uint32_t first, int nsweeps, int every, double* trace, pmc_stats* st) {
+    if (every < 1) return PMC_ERR_ARG;
+    int rc = PMC_OK;
+    for (int k = 0; k + every <= nsweeps; k += every) {
+        const int r = orc_run(p, disk, n, sdisk, sn, first + (uint32_t)k, every, st);
+        if (r) rc = r;
+        trace[k / every] = orc_energy(p, disk, n);
+    }
+    return rc;
+}
+
 /* ------------------------------------------------------------------------------------- */
 /* primitives for tests                                                                  */
 /* ------------------------------------------------------------------------------------- */

@@ -11,8 +11,9 @@
  * be built here (CUDA + cuRAND absent; building it would need stand-in headers, which this
  * project does not write), so the oracle is pinned by the reference's own data file
  * CUDA-Parallel-MC/CUDA-Parallel-MC/dumpR3.txt (lattice + energy function), by the lattice
- * energies derived from its definitions, by published Philox KATs and by the statistical
- * known answer <E> = -21.240 +- 0.022 of the N=64 model.  The cuRAND XORWOW trajectory of the
+ * energies derived from its definitions, by published Philox KATs and by statistical known
+ * answers of <E> from an independent textbook Metropolis code (tools/textbook_mc.c,
+ * tests/golden/known_answers.json: N=64 and N=305 particles in L=10, the configs' density).  The cuRAND XORWOW trajectory of the
  * reference is intentionally not reproduced (parity unpinned for the exact stream).
  */
 #ifndef PMC_ORACLE_H
@@ -52,6 +53,10 @@ double orc_energy(const pmc_params* p, const float* disk, const int16_t* n);
  * (disk, n) -- scratch buffers of the same size are used for the shift ping-pong */
 int orc_run(const pmc_params* p, float* disk, int16_t* n, float* sdisk, int16_t* sn,
             uint32_t first, int nsweeps, pmc_stats* st);
+
+/* orc_run recording the cell-list energy after every `every`-th sweep (trace[nsweeps / every]) */
+int orc_run_trace(const pmc_params* p, float* disk, int16_t* n, float* sdisk, int16_t* sn,
+                  uint32_t first, int nsweeps, int every, double* trace, pmc_stats* st);
 
 /* exported primitives for unit tests */
 void orc_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);

@@ -80,6 +80,8 @@ def lib():
         L.orc_energy.argtypes = [P, _f32p, _i16p]
         L.orc_energy.restype = C.c_double
         L.orc_run.argtypes = [P, _f32p, _i16p, _f32p, _i16p, C.c_uint32, C.c_int, C.POINTER(Stats)]
+        L.orc_run_trace.argtypes = [P, _f32p, _i16p, _f32p, _i16p, C.c_uint32, C.c_int, C.c_int,
+                                    np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS"), C.POINTER(Stats)]
         L.orc_philox.argtypes = [C.POINTER(C.c_uint32 * 4), C.POINTER(C.c_uint32 * 2),
                                  C.POINTER(C.c_uint32 * 4)]
         L.orc_philox.restype = None
@@ -157,6 +159,17 @@ class OracleState:
         sn = self.n.copy()
         return lib().orc_run(C.byref(self.p), self.disk, self.n, sd, sn, first, nsweeps,
                              C.byref(self.stats))
+
+    def run_trace(self, first: int, nsweeps: int, every: int) -> np.ndarray:
+        """run(first, nsweeps) recording the energy after every `every`-th sweep (one C call)."""
+        sd = self.disk.copy()
+        sn = self.n.copy()
+        tr = np.zeros(nsweeps // every, np.float64)
+        rc = lib().orc_run_trace(C.byref(self.p), self.disk, self.n, sd, sn, first, nsweeps, every, tr,
+                                 C.byref(self.stats))
+        if rc:
+            raise RuntimeError(f"orc_run_trace: rc={rc}")
+        return tr
 
     # --- views --------------------------------------------------------------------------
     def disk3(self) -> np.ndarray:

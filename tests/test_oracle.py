@@ -1,6 +1,7 @@
 """CPU tests of the oracle: pinned against the reference's own data file (dumpR3.txt frames),
-lattice energies derived from the reference's definitions, published Philox KATs and the
-statistical known answer of the N=64 model."""
+lattice energies derived from the reference's definitions, published Philox KATs and statistical
+known answers of an independent textbook Metropolis code (tests/golden/known_answers.json)."""
+import json
 import math
 import os
 
@@ -239,26 +240,78 @@ def test_energy_bookkeeping(oracle):
     assert int(st.n.sum()) == 2000
 
 
-@pytest.mark.parametrize("flags", [0, 1])
-def test_mean_energy_known_answer(oracle, flags):
-    """<E> of the N=64, L=10, beta=0.3, sigma=0.5, rc=2.5 model: -21.240 +- 0.022 (textbook
-    Metropolis).  The checkerboard chain must sample the same distribution,
-    with the default z-parity-grouped colour order and with the full shuffle (flags=1).
-    Tolerance: 3 sigma of (block SE of this run, SE of the known answer) plus a flat 0.02 -- the
-    reference's own chain cannot be reproduced (cuRAND XORWOW, re-seeded per launch:
-    subsweep.h:256-259), so this statistical pin is the strongest one the reference allows for the
-    move/accept chain (accept rule subsweep.h:209-216)."""
-    st = oracle.OracleState(oracle.make_params(cps=4, flags=flags))
-    st.init_lattice(64)
-    st.run(0, 500)
-    es = []
-    for s in range(500, 30500, 5):
-        st.run(s, 5)
-        es.append(st.energy())
-    es = np.array(es)
-    blocks = es.reshape(20, -1).mean(1)
-    se = blocks.std(ddof=1) / np.sqrt(len(blocks))
-    assert abs(es.mean() - (-21.240)) < 3 * math.hypot(se, 0.022) + 0.02
+def _known_answer(name):
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "known_answers.json")
+    with open(path) as f:
+        return json.load(f)["models"][name]
+
+
+def _oracle_mean_energy(oracle, n_atoms, flags, equil, sweeps, every=5, chains=8, blocks=20):
+    """<E> of `chains` independent oracle chains (Philox seeds 1000..) of the 4^3-cell box (L = 10)
+    in threads (the C calls release the GIL): every chain equilibrates `equil` sweeps from the
+    lattice, then records the energy after every `every`-th sweep; the standard error is that of the
+    pooled batch means (`blocks` per chain)."""
+    import threading
+    res = [None] * chains
+
+    def chain(k):
+        st = oracle.OracleState(oracle.make_params(cps=4, seed=1000 + k, flags=flags))
+        assert st.init_lattice(n_atoms) == 0
+        assert st.run(0, equil) == 0
+        res[k] = st.run_trace(equil, sweeps, every)
+
+    th = [threading.Thread(target=chain, args=(k,)) for k in range(chains)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    bm = np.concatenate([r.reshape(blocks, -1).mean(1) for r in res])
+    return float(bm.mean()), float(bm.std(ddof=1) / np.sqrt(len(bm)))
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("model,n_atoms,flags,sweeps", [
+    ("n64", 64, 0, 60_000),
+    ("n64", 64, 1, 60_000),      # the reference-like full colour shuffle
+    ("n305", 305, 0, 20_000),    # 4.77 particles per cell: the density of BASELINE configs 3-5
+])
+def test_mean_energy_known_answer(oracle, model, n_atoms, flags, sweeps):
+    """The oracle's move/shuffle/accept/shift chain samples the Boltzmann distribution of the
+    reference's model: its <E> equals the known answer of an INDEPENDENT textbook Metropolis code
+    (tools/textbook_mc.c: no cells, full minimum image, truncated LJ subsweep.h:90-103, accept rule
+    subsweep.h:209-216; tests/golden/known_answers.json from tools/make_known_answers.py, 8 seeds
+    each: N=64 -21.262 +- 0.007, N=305 -477.64 +- 0.08 in L=10, beta=0.3, sigma=0.5, rc=2.5).
+    Tolerance: 3 sigma of the combined standard error (this run's pooled batch means, the known
+    answer's), no flat allowance: 0.24-0.26% of <E> at N=64, 0.10% at N=305.  The GPU equals the oracle
+    bit for bit, so this pins the GPU chain too.  The reference's own chain cannot be reproduced
+    (cuRAND XORWOW re-seeded per launch, subsweep.h:256-259)."""
+    ka = _known_answer(model)
+    assert ka["N"] == n_atoms and ka["se_rel"] <= 0.003
+    mean, se = _oracle_mean_energy(oracle, n_atoms, flags, equil=1000 if n_atoms == 64 else 2000, sweeps=sweeps)
+    tol = 3.0 * math.hypot(se, ka["se"])
+    assert abs(mean - ka["mean"]) < tol, (mean, se, ka["mean"], ka["se"])
+    assert tol < 0.003 * abs(ka["mean"])
+
+
+def test_known_answer_tool_reproduces(tmp_path):
+    """tools/textbook_mc.c is the committed generator of the known answers: it builds and, for the
+    first seed of the N=64 model over a short window, lands within 5 of its own standard errors of
+    the committed pooled answer; the committed file names the tool's current source hash."""
+    import hashlib
+    import subprocess
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = os.path.join(repo, "tools", "textbook_mc.c")
+    with open(os.path.join(repo, "tests", "golden", "known_answers.json")) as f:
+        ka_all = json.load(f)
+    assert ka_all["tool_sha256"] == hashlib.sha256(open(src, "rb").read()).hexdigest()
+    exe = str(tmp_path / "textbook_mc")
+    subprocess.run(["gcc", "-O2", "-std=c11", "-o", exe, src, "-lm"], check=True)
+    ka = ka_all["models"]["n64"]
+    out = subprocess.run([exe, "64", "10", "0.3", "0.5", "2.5", "1000", "10000", "10", "101"],
+                         capture_output=True, text=True, check=True).stdout
+    r = json.loads(out)
+    assert abs(r["mean"] - ka["mean"]) < 5 * math.hypot(r["se"], ka["se"])
+    assert 0.80 < r["acceptance"] < 0.83
 
 
 def test_subsweep_range_split_equals_full(oracle):
