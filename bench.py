@@ -1,12 +1,14 @@
 """bench.py -- MC trial-moves/s of the checkerboard Metropolis hot path on MI355X.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 3|4|5|5box]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5|5box]
   torchrun --nproc-per-node N bench.py --gpus N ...     (one rank per GPU, z-slab decomposition)
 
 A "step" is one full MC sweep (8 checkerboard colour phases + shiftCells) with the state resident
 in HBM; w=rc=2.5, beta=0.3, sigma=0.5, n_M=10, nmax=16, Philox seed 1234, reference lattice start
 (kernel.cu:78-89).  The workloads are BASELINE.json's configs:
 
+  2                       64^3 cells, 1e6 particles, 1 GPU, single-colour sweep: a step is ONE colour
+                          phase (step k: colour k % 8 at sweep index k // 8, no shiftCells).
   3     (default at N=1)  128^3 cells, 1e7 particles, 1 GPU, whole periodic box.
   4     (default at N>1)  the SAME 128^3 / 1e7 box split into N z-slabs of 128/N planes (strong
                           scaling; the C slab driver, halo planes over RCCL).  N=1 runs config 3.
@@ -38,6 +40,8 @@ sys.path.insert(0, os.path.join(REPO, "parallel-monte-carlo_amd"))
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 CONFIG_NAMES = {
+    "2": "BASELINE config 2: 64^3 cells, 1e6 particles, 1 MI355X, single-colour sweep (a step is one colour "
+         "phase: colour k % 8 at sweep index k // 8, no shiftCells)",
     "3": "BASELINE config 3: 128^3 cells, 1e7 particles, 1 MI355X, full checkerboard + shiftCells",
     "4": "BASELINE config 4: 128^3 cells, 1e7 particles, {n} MI355X, checkerboard domain decomposition "
          "+ RCCL halo (strong scaling: {n} z-slabs of {nz} planes)",
@@ -123,12 +127,14 @@ def host_cpu() -> dict:
             "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
 
 
-def cpu_baseline(disk, n, cps: int, sweep0: int, serial_planes: int, cps_z: int = 0) -> tuple[dict, object]:
+def cpu_baseline(disk, n, cps: int, sweep0: int, serial_planes: int, cps_z: int = 0,
+                 phase: tuple[int, int] | None = None) -> tuple[dict, object]:
     """The C oracle (the reference has no CPU path: SURVEY.md 0/8c) timed on this host:
     (i) serial, one core: one colour phase over planes [0, serial_planes);
     (ii) OpenMP over the cells of a colour on the cores of one socket (one thread per physical
     core, limited by the CPUs/cgroup quota this process may use): one full sweep from the GPU
-    state.  Returns the JSON object and the oracle state after (ii) for the parity leg."""
+    state, or with phase = (colour, sweep index) that one colour phase of the whole box (config 2).
+    Returns the JSON object and the oracle state after (ii) for the parity leg."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import pmc_oracle  # test infrastructure: timed CPU baseline only
     pmc_oracle.build()
@@ -142,8 +148,10 @@ def cpu_baseline(disk, n, cps: int, sweep0: int, serial_planes: int, cps_z: int 
     st1.n[:] = n
     pmc_oracle.set_threads(1)
     import ctypes as C
+    o1 = pmc_oracle.colour_offset(phase[0]) if phase else (0, 0, 0)
+    s1 = phase[1] if phase else sweep0
     t0 = time.perf_counter()
-    pmc_oracle.lib().orc_subsweep_range(C.byref(st1.p), st1.disk, st1.n, 0, 0, 0, sweep0, 0, serial_planes,
+    pmc_oracle.lib().orc_subsweep_range(C.byref(st1.p), st1.disk, st1.n, o1[0], o1[1], o1[2], s1, 0, serial_planes,
                                         C.byref(st1.stats))
     dt1 = time.perf_counter() - t0
     serial = st1.stats.trials / dt1
@@ -159,12 +167,16 @@ def cpu_baseline(disk, n, cps: int, sweep0: int, serial_planes: int, cps_z: int 
     st.n[:] = n
     used = pmc_oracle.set_threads(threads)
     t0 = time.perf_counter()
-    st.run(sweep0, 1)
+    if phase:
+        st.subsweep(pmc_oracle.colour_offset(phase[0]), phase[1])
+    else:
+        st.run(sweep0, 1)
     dt = time.perf_counter() - t0
     par = st.stats.trials / dt
     cores_socket = host["cores_per_socket"] or threads
+    what = (f"colour phase {phase[0]} (sweep index {phase[1]})" if phase else "full sweep")
     out = {"value": par, "unit": "trial-moves/s", "cores": threads, "kind": "port",
-           "sample": f"one full sweep of the {box} box from the GPU state, C oracle, OpenMP over the cells "
+           "sample": f"one {what} of the {box} box from the GPU state, C oracle, OpenMP over the cells "
                      f"of a colour on {threads} threads (one per physical core of socket 0; limited by "
                      f"{limited_by}), {dt:.2f} s",
            "serial": {"value": serial, "cores": 1,
@@ -325,7 +337,7 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", choices=["3", "4", "5", "5box"], default=None,
+    ap.add_argument("--config", choices=["2", "3", "4", "5", "5box"], default=None,
                     help="BASELINE config (default: 3 at N=1, 4 at N>1)")
     ap.add_argument("--strong", action="store_true", help="alias of --config 4")
     ap.add_argument("--cps", type=int, default=None, help="override cells per side (configs 3/4)")
@@ -350,7 +362,12 @@ def main() -> int:
     ap.add_argument("--emulate-ranks", type=int, default=0,
                     help="config 4 at N=1: one rank's slab of an R-rank run (the bottom 128/R planes of the "
                          "1e7 lattice as a periodic slab) -- the per-rank launch shapes, for rocprof")
+    ap.add_argument("--xfer-delay-us", type=float, default=0.0,
+                    help="slab rehearsals: hold the exchange stream busy this long after every halo exchange "
+                         "(PMC_XFER_DELAY_US: the xGMI time and RCCL latency a one-GPU run does not pay)")
     args = ap.parse_args()
+    if args.xfer_delay_us > 0:
+        os.environ["PMC_XFER_DELAY_US"] = str(args.xfer_delay_us)   # read by libpmc at its first exchange
 
     import torch
     import torch.distributed as dist
@@ -368,8 +385,8 @@ def main() -> int:
         args.slab = True
     if config == "4" and world == 1 and not args.slab:
         config = "3"          # the 1-GPU point of the config-4 strong-scaling curve is config 3
-    if config == "5box" and world > 1:
-        raise SystemExit("--config 5box is the single-GPU 256^3 box")
+    if config in ("2", "5box") and world > 1:
+        raise SystemExit(f"--config {config} is a single-GPU configuration")
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -380,7 +397,10 @@ def main() -> int:
         if world > 1:
             dist.barrier()
 
-    if config in ("3", "4"):
+    if config == "2":
+        cps = args.cps or 64
+        atoms = args.atoms or 1_000_000
+    elif config in ("3", "4"):
         cps = args.cps or 128
         atoms = args.atoms or 10_000_000
     else:
@@ -406,12 +426,16 @@ def main() -> int:
         from pmc_amd.plan import sweep_plan
         plans = {}
 
-        def one_sweep(s):
-            if s not in plans:
-                plans[s] = sweep_plan(1234, s, 2.5)
-            for colour in plans[s][0]:
-                sim.phase(colour, s)
-            sim.shift(s)
+        if config == "2":
+            def one_sweep(s):       # config 2's step: ONE colour phase, colour s % 8 at sweep s // 8
+                sim.phase(s % 8, s // 8)
+        else:
+            def one_sweep(s):
+                if s not in plans:
+                    plans[s] = sweep_plan(1234, s, 2.5)
+                for colour in plans[s][0]:
+                    sim.phase(colour, s)
+                sim.shift(s)
 
         def finish():
             pass
@@ -444,7 +468,21 @@ def main() -> int:
     # algorithmic bytes from the state at the start of the timed region
     disk_h, n_h = sim.copy_out()
     plane = cps * cps
-    if not slab:
+    if config == "2":
+        # the timed steps' colours (no shiftCells: the counts, hence the bytes, stay fixed)
+        n_owned = n_h.astype(np.int64)
+        stencil = stencil_counts(n_owned, (cps, cps, cps))
+        idx = np.arange(cps ** 3)
+        cx, cy, cz = idx % cps, (idx // cps) % cps, idx // (cps * cps)
+        per_colour = []
+        for colour in range(8):
+            o = (colour // 4) % 2, (colour // 2) % 2, colour % 2     # itoa, start.cu:153-157
+            m = (cx % 2 == o[0]) & (cy % 2 == o[1]) & (cz % 2 == o[2])
+            per_colour.append(staged_bytes(n_owned[m], stencil[m]))
+        timed = [per_colour[(args.warmup + k) % 8] for k in range(args.steps)]
+        sub_launch_bytes = float(np.mean(timed))
+        roof_kernel = "k_subsweep<16,16,true> (one colour phase of the 64^3 box; mean over the timed steps' colours)"
+    elif not slab:
         n_owned = n_h.astype(np.int64)
         stencil = stencil_counts(n_owned, (cps, cps, cps))
         sub_launch_bytes = staged_bytes(n_owned, stencil) / 8.0
@@ -452,14 +490,10 @@ def main() -> int:
     else:
         n_owned = n_h[plane:plane * (nz_local + 1)].astype(np.int64)
         stencil = slab_stencil_counts(n_h, cps, nz_local)
-        # kind-0 launches: the two interior chains, planes [1, zs) and [zs, nz-1) (pmc_slab_sweep;
-        # one chain when zs < 2 or PMC_SLAB_CHAINS=1), one launch per chain and colour phase; the
-        # roofline's bytes per launch are their mean (the chains run concurrently)
-        zs = 2 * (nz_local // 4)
-        if zs < 2 or os.environ.get("PMC_SLAB_CHAINS") == "1":
-            zs = nz_local - 1
-        chains = [(1, zs)] + ([(zs, nz_local - 1)] if nz_local - 1 > zs else [])
-        chains = [(a, b) for a, b in chains if b > a]
+        # kind-0 launches: the interior chains (pmc_slab_layout: 1-3 chains, PMC_SLAB_CHAINS), one
+        # launch per chain and colour phase; the roofline's bytes per launch are their mean (the
+        # chains run concurrently)
+        chains = [(a, b) for a, b in drv.ctx.slab_layout() if b > a]
         per_chain = [staged_bytes(n_owned[a * plane:b * plane], stencil[a * plane:b * plane]) / 8.0
                      for a, b in chains]
         sub_launch_bytes = sum(per_chain) / len(per_chain) if per_chain else 0.0
@@ -549,8 +583,12 @@ def main() -> int:
         if not slab:
             if rank == 0:
                 try:
-                    cpu, ost = cpu_baseline(disk_h, n_h, cps, first, sp)
+                    ph = (first % 8, first // 8) if config == "2" else None
+                    cpu, ost = cpu_baseline(disk_h, n_h, cps, first, sp, phase=ph)
                     parity = parity_leg(sim, one_sweep, disk_h, n_h, first, 1, e_start, ost)
+                    if config == "2":
+                        parity["sweeps"] = 0
+                        parity["phase"] = {"colour": first % 8, "sweep_index": first // 8}
                 except Exception as e:  # the baseline is reported, never the measured value
                     cpu = {"error": repr(e)}
         else:
@@ -571,7 +609,7 @@ def main() -> int:
                 parity = parity_leg_slab(sim, one_sweep, finish, disk_h, n_h, first, e_start, gather, ost, rank)
 
     if rank == 0:
-        sweeps_per_s = args.steps / elapsed
+        sweeps_per_s = args.steps / elapsed / (8.0 if config == "2" else 1.0)
         name = CONFIG_NAMES[config].format(n=world, nz=nz_local, cz=box_z)
         if args.emulate_ranks:
             name = (f"rehearsal of BASELINE config 4 at {args.emulate_ranks} ranks on 1 MI355X: one rank's slab "
@@ -585,6 +623,7 @@ def main() -> int:
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
+            **({"step": "one colour phase"} if config == "2" else {}),
             "higher_is_better": True,
             # configs 3 -> 4 are one fixed box over 1..N GPUs (strong); config 5 fixes the work per GPU
             "scaling": "weak" if config == "5" else "strong",
@@ -597,7 +636,8 @@ def main() -> int:
             "config": {"workload": name, "baseline_config": config,
                        "box_cells": [cps, cps, box_z], "cells_per_gpu": cps * cps * nz_local,
                        "particles": particles, "n_moves": 10, "nmax": 16, "beta": 0.3, "sigma": 0.5,
-                       "w": 2.5, "parallelism": transport},
+                       "w": 2.5, "parallelism": transport,
+                       **({"injected_exchange_delay_us": args.xfer_delay_us} if args.xfer_delay_us > 0 else {})},
             "sweeps_per_s": sweeps_per_s,
             "acceptance": accepted_total / trials_total if trials_total else None,
             "energy": {"start": e_start, "end": e_end, "start_plus_sum_dE": e_start + de_timed,

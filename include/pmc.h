@@ -144,7 +144,7 @@ int pmc_shift(pmc_ctx* ctx, uint32_t sweep);
 /* Slab contexts (halo = 1) after the 8 phases of a sweep, when both halo planes are exact copies
  * of the neighbours' boundary planes: the sweep plan's shiftCells over the owned planes AND every
  * halo plane whose new content depends only on planes this rank holds (along x/y both halos, along
- * z in direction dir the one on the -dir side; shiftCells.h:46-108 applied to the halo copies, the
+ * z in direction dir the one on the -dir side; VS shiftCells.h:38-108 applied to the halo copies, the
  * same float operations as the plane's owner), then the buffer swap.  *halo_recv tells the caller
  * which halo still has to be received: 0 none, +1 the top halo (local plane nz_local) from the rank
  * above's new plane 0, -1 the bottom halo (plane -1) from the rank below's new top plane.  The C
@@ -166,10 +166,11 @@ int pmc_phase_range_on(pmc_ctx* ctx, int colour, uint32_t sweep, int zl_begin, i
  * rank r owns planes [r*nz_local, (r+1)*nz_local) of a cps_x x cps_y x (world*nz_local) periodic
  * box (context created with halo = 1, z0 = r*nz_local) plus a halo plane below and above.  The
  * whole sweep schedule runs in C.  The 8 colour phases of a sweep form runs of equal z parity q (two
- * runs of 4 with the default order); each run is three independent launch chains: the interior
- * planes in two chains (context stream and a second stream) and the boundary plane of parity q on
- * the exchange stream, which then sends that whole plane to the neighbour holding it as a halo and
- * receives the opposite halo (one RCCL send/recv each way per run) while the interior chains run.
+ * runs of 4 with the default order); each run is independent launch chains: the interior planes
+ * in 1-3 chains (PMC_SLAB_CHAINS, default 2: the context stream and one or two more streams) and
+ * the boundary plane of parity q on the exchange stream, which then sends that whole plane to the
+ * neighbour holding it as a halo and receives the opposite halo (one RCCL send/recv each way per
+ * run) while the interior chains run.
  * After shiftCells only a z shift needs one more plane (with its counts) from one side.  Every rank
  * derives the sweep plan itself and RNG counters use global cell ids, so any world size
  * reproduces the single-GPU run bit for bit.  librccl is dlopen'ed ("librccl.so.1", or the path
@@ -201,6 +202,9 @@ int pmc_slab_exchange(pmc_ctx* ctx);
 int pmc_slab_sweep(pmc_ctx* ctx, uint32_t sweep);
 /* Order the context stream after the outstanding exchanges (before reading state or halos). */
 int pmc_slab_finish(pmc_ctx* ctx);
+/* The interior chains of pmc_slab_sweep: *n_chains chains, chain j over local planes
+ * [borders[j], borders[j+1]) (borders[0] = 1, borders[*n_chains] = nz_local - 1). */
+int pmc_slab_layout(pmc_ctx* ctx, int* n_chains, int borders[4]);
 /* Observables of the whole box (one sum over the ranks per report): the four counters
  * (pmc_stats_read without reset) and, with with_energy, the cell-list energy (pmc_energy), each
  * summed over all ranks in fixed point -- exact, equal to a one-GPU run's -- through the slab's
@@ -213,9 +217,8 @@ int pmc_slab_observables(pmc_ctx* ctx, int with_energy, pmc_stats* out, double* 
  * overflow (fallback) launches are not timed.  pmc_timing reports the kind-[0] subsweep launches and
  * the shift launches; pmc_slab_timing is the same call, requiring the slab driver.
  * pmc_timing_kinds splits by kind: [0] subsweep launches of whole colour phases or of a slab's
- * interior planes (the slab driver's two interior chains, planes [1, zs) on the context stream and
- * [zs, nz_local-1) on a second stream, zs = 2*floor(nz_local/4): two launches per phase, running
- * concurrently), [1] shiftCells, [2] the slab driver's boundary-plane launches and
+ * interior planes (the slab driver's interior chains, pmc_slab_layout: one launch per chain and
+ * phase, running concurrently), [1] shiftCells, [2] the slab driver's boundary-plane launches and
  * pmc_phase_range_on launches (other streams: they overlap [0], durations do not add). */
 int pmc_timing(pmc_ctx* ctx, int enable, double* subsweep_ms, int* n_subsweep, double* shift_ms, int* n_shift);
 int pmc_timing_kinds(pmc_ctx* ctx, int enable, double ms[3], int count[3]);
@@ -243,9 +246,10 @@ int pmc_run_graph(pmc_ctx* ctx, uint32_t first_sweep, int count);
  * first..first+count-1 as ONE launch per 32 sweeps on one XCD, in-kernel barriers where the 17
  * launches of a sweep were (start.cu:242-249's per-phase launch + synchronize); identical results
  * to pmc_sweep in a loop.  PMC_ERR_ARG for a box that does not qualify.  One XCD is an eighth of the
- * chip: faster than per-phase launches only for tiny boxes, so pmc_start uses it for boxes of at
- * most 64 cells per colour (PMC_SMALL=0 in the environment: never).  Error flags bit 3: a
- * barrier timed out; bit 4: the launch's blocks were not dealt round-robin over the XCDs. */
+ * chip: slower than per-phase launches (16^3: 0.513 against 0.072 ms per sweep), so pmc_start does
+ * not use it by default (PMC_SMALL=1 in the environment: for boxes of at most 64 cells per colour).
+ * Error flags bit 3 (value 8): a barrier timed out; bit 4 (value 16): the launch's blocks were not
+ * dealt round-robin over the XCDs; bit 5 (value 32): no workgroup of the launch ran on XCD 0. */
 int pmc_run_small(pmc_ctx* ctx, uint32_t first_sweep, int count);
 
 /* ---- observables ------------------------------------------------------------------- */

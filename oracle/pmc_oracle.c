@@ -363,8 +363,8 @@ int orc_shift_cells_planes(const pmc_params* p, const float* din, const int16_t*
     const float w = p->w;
     const int cps[3] = {p->cps_x, p->cps_y, p->cps_z};
     const float Lf = (float)cps[f] * w;
-    const int dir = (d <= 0) ? -1 : 1;               /* shiftCells.h:46-53 */
-    const float s = w * (float)dir;                  /* float s (fixed copy :28,84) */
+    const int dir = (d <= 0) ? -1 : 1;               /* VS shiftCells.h:38-44 */
+    const float s = w * (float)dir;                  /* float s (VS copy :28, :83-85) */
     const int64_t total = (int64_t)p->cps_x * p->cps_y * (zl_end - zl_begin);
     int over = 0;
 #ifdef _OPENMP
@@ -377,8 +377,8 @@ int orc_shift_cells_planes(const pmc_params* p, const float* din, const int16_t*
         int cid[3] = {x, y, p->z0 + zl};
         if (cid[2] < 0) cid[2] += p->cps_z; else if (cid[2] >= p->cps_z) cid[2] -= p->cps_z;
         int64_t c = sidx(p, x, y, zl);
-        float offset = (float)cid[f] * w - Lf / 2.0f;   /* :55 */
-        /* neighbour in direction of f (:82-96) */
+        float offset = (float)cid[f] * w - Lf / 2.0f;   /* VS :46 */
+        /* neighbour in direction of f (VS :73-88) */
         int nb[3] = {x, y, zl};
         int nbg = cid[f] + dir;
         if (nbg < 0) nbg = cps[f] - 1; else if (nbg >= cps[f]) nbg = 0;
@@ -388,7 +388,7 @@ int orc_shift_cells_planes(const pmc_params* p, const float* din, const int16_t*
         float offset_nb = (float)nbg * w - Lf / 2.0f;
         int ncur = nin[c], nnb = nin[cnb];
         int nnew = 0;
-        for (int i = 0; i < ncur; ++i) {                 /* :66-80 */
+        for (int i = 0; i < ncur; ++i) {                 /* VS :52-71 */
             float D = (din[c * 3 * nm + f * nm + i] - offset) - d;
             if (D > 0 && D <= w) {
                 if (nnew < nm)
@@ -398,7 +398,7 @@ int orc_shift_cells_planes(const pmc_params* p, const float* din, const int16_t*
                 ++nnew;
             }
         }
-        for (int i = 0; i < nnb; ++i) {                  /* :97-111 */
+        for (int i = 0; i < nnb; ++i) {                  /* VS :90-102 */
             float D = (din[cnb * 3 * nm + f * nm + i] - offset_nb) - d;
             if (!(D > 0 && D <= w)) {
                 if (nnew < nm)

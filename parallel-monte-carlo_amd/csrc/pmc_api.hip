@@ -37,6 +37,7 @@ struct pmc_ctx {
     int* ovf = nullptr;                    // subsweep overflow queue (1 + cells per colour)
     int* ovf_aux = nullptr;                // second queue: launches on a caller stream (pmc_phase_range_on)
     int* ovf_b = nullptr;                  // third queue: the slab driver's boundary chain
+    int* ovf_aux2 = nullptr;               // fourth queue: the slab driver's third interior chain
     size_t ovf_bytes = 0;
     int32_t* tmp_cnt = nullptr;
     int32_t* tmp_idx = nullptr;
@@ -281,6 +282,7 @@ void pmc_destroy(pmc_ctx* c) {
     if (c->ovf) (void)hipFree(c->ovf);
     if (c->ovf_aux) (void)hipFree(c->ovf_aux);
     if (c->ovf_b) (void)hipFree(c->ovf_b);
+    if (c->ovf_aux2) (void)hipFree(c->ovf_aux2);
     if (c->tmp_cnt) (void)hipFree(c->tmp_cnt);
     if (c->tmp_idx) (void)hipFree(c->tmp_idx);
     if (c->d_r) (void)hipFree(c->d_r);
@@ -603,17 +605,37 @@ int pmc_run_small(pmc_ctx* c, uint32_t first, int count) {
     if (small_sweep_participants(c->G) == 0)
         return fail(PMC_ERR_ARG, "pmc_run_small: the box does not qualify (whole box, nmax 16, <= 2048 cells per colour)");
     if (count == 0) return PMC_OK;
-    // barrier counter: flags word 2 (word 0 holds the error bits)
-    hipError_t e = launch_sweep_small(c->G, c->disk[0], c->n[0], c->disk[1], c->n[1], c->cur, c->stats, c->flags,
-                                      (unsigned*)(c->flags + 2), c->P.seed, first, count, c->P.flags, c->stream);
-    if (e != hipSuccess) return hip_fail(e, "small-box sweep launch");
-    if (count & 1) c->cur ^= 1;
+    const unsigned P = (unsigned)small_sweep_participants(c->G);
+    // one launch per kSmallSweeps sweeps; after each, the barrier counter (flags word 2; word 0 holds
+    // the error bits) must show every participant at every one of the launch's 9 barriers per sweep.
+    // A launch none of whose workgroups ran on XCD 0 (the kernel's participation test) does nothing
+    // and reaches no barrier: without this check the context would flip to the stale buffer.
+    for (int done = 0; done < count;) {
+        const int n = count - done < kSmallSweeps ? count - done : kSmallSweeps;
+        hipError_t e = launch_sweep_small(c->G, c->disk[0], c->n[0], c->disk[1], c->n[1], c->cur, c->stats, c->flags,
+                                          (unsigned*)(c->flags + 2), c->P.seed, first + (uint32_t)done, n, c->P.flags,
+                                          c->stream);
+        if (e != hipSuccess) return hip_fail(e, "small-box sweep launch");
+        uint32_t w[3] = {0, 0, 0};
+        PMC_HIP(hipMemcpyAsync(w, c->flags, sizeof w, hipMemcpyDeviceToHost, c->stream));
+        PMC_HIP(hipStreamSynchronize(c->stream));
+        if (w[0] & 8u) return fail(PMC_ERR_HIP, "small-box sweep: a barrier timed out (participants not co-resident)");
+        if (w[0] & 16u) return fail(PMC_ERR_HIP, "small-box sweep: the launch was not dealt round-robin over the XCDs");
+        if (w[2] != 9u * P * (unsigned)n) {
+            w[0] |= 32u;
+            PMC_HIP(hipMemcpyAsync(c->flags, &w[0], sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+            PMC_HIP(hipStreamSynchronize(c->stream));
+            return fail(PMC_ERR_HIP, "small-box sweep: no workgroup of the launch ran on XCD 0 (state unchanged)");
+        }
+        if (n & 1) c->cur ^= 1;
+        done += n;
+    }
     return PMC_OK;
 }
 
 // pmc_start runs every box with eager launches: since small colour phases run as one full-capacity
 // launch each (k_subsweep_full, 9 launches per sweep), they beat pmc_run_small's single launch on
-// XCD 0 at every size (8^3: 0.070 against 0.110 ms per sweep, 16^3: 0.072 against 0.70 ms,
+// XCD 0 at every size (8^3: 0.070 against 0.110 ms per sweep, 16^3: 0.072 against 0.513 ms,
 // profiles/r03sm_small_box.txt; round 3 had picked pmc_run_small for <= 64 cells per colour against
 // the 17-launch sweep).  PMC_SMALL=1 restores that choice; pmc_run_small stays callable.
 static bool use_small(const pmc_ctx* c) {
@@ -666,6 +688,7 @@ int pmc_start_ex(pmc_ctx* c, uint32_t first, int mc_passes, int flags, pmc_resul
     if (fl & 1u) return fail(PMC_ERR_OVERFLOW, "shiftCells: cell occupancy exceeded nmax");
     if (fl & 8u) return fail(PMC_ERR_HIP, "small-box sweep: a barrier timed out (participants not co-resident)");
     if (fl & 16u) return fail(PMC_ERR_HIP, "small-box sweep: the launch was not dealt round-robin over the XCDs");
+    if (fl & 32u) return fail(PMC_ERR_HIP, "small-box sweep: no workgroup of the launch ran on XCD 0");
     return PMC_OK;
 }
 
@@ -961,11 +984,18 @@ struct pmc_slab {
     ncclComm_t comm = nullptr;            // RCCL transport
     pmc_local_group* group = nullptr;     // in-process transport (not owned)
     hipStream_t aux = nullptr;            // halo exchanges ("T")
-    hipStream_t hi = nullptr;             // the upper plane chain (two-chain schedule)
-    int chains = 1;                       // plane chains (streams running subsweeps): 1 or 2
+    hipStream_t hi[2] = {nullptr, nullptr};   // interior chains 1 and 2 (chain 0 runs on the context stream)
+    int chains = 2;                       // interior plane chains (streams running subsweeps): 1, 2 or 3
     hipEvent_t ev_i = nullptr, ev_b = nullptr, ev_t = nullptr;
     hipEvent_t ev_x = nullptr;            // T after its latest exchange
-    hipEvent_t ev_run[3][2] = {{nullptr, nullptr}, {nullptr, nullptr}, {nullptr, nullptr}};   // [L, U, B][parity]
+    static constexpr int kB = 3;          // chain index of the boundary chain (T)
+    hipEvent_t ev_run[4][2] = {};         // [interior chain 0..2, boundary][parity]
+    std::vector<hipEvent_t*> run_events() {
+        std::vector<hipEvent_t*> v;
+        for (auto& r : ev_run)
+            for (auto& e : r) v.push_back(&e);
+        return v;
+    }
     std::vector<XferMsg> sends, recvs;    // the exchange being assembled
     bool messages() const { return comm != nullptr || group != nullptr; }
 };
@@ -982,13 +1012,36 @@ void drop_slab(pmc_ctx* c) {
         s->group->slot[s->rank].joined = false;
     }
     if (s->aux) (void)hipStreamDestroy(s->aux);
-    if (s->hi) (void)hipStreamSynchronize(s->hi);
-    for (hipEvent_t e : {s->ev_i, s->ev_b, s->ev_t, s->ev_x, s->ev_run[0][0], s->ev_run[0][1], s->ev_run[1][0],
-                         s->ev_run[1][1], s->ev_run[2][0], s->ev_run[2][1]})
+    for (hipStream_t h : s->hi)
+        if (h) (void)hipStreamSynchronize(h);
+    for (hipEvent_t e : {s->ev_i, s->ev_b, s->ev_t, s->ev_x})
         if (e) (void)hipEventDestroy(e);
-    if (s->hi) (void)hipStreamDestroy(s->hi);
+    for (hipEvent_t* e : s->run_events())
+        if (*e) (void)hipEventDestroy(*e);
+    for (hipStream_t h : s->hi)
+        if (h) (void)hipStreamDestroy(h);
     delete s;
     c->slab = nullptr;
+}
+
+// Interior plane chains of a slab of nz planes: chain j covers planes [zs[j], zs[j+1]) of the
+// interior [1, nz-1); every inner border is even (a parity-q run of a chain then ends at the same
+// side of each border).  Two chains split at 2*(nz/4), three at the even planes nearest 1/3 and
+// 2/3 of the interior; degenerate splits of thin slabs fold into fewer chains.  Returns the count.
+int slab_split(int chains, int nz, int zs[4]) {
+    zs[0] = 1;
+    zs[1] = zs[2] = zs[3] = nz - 1;
+    if (chains == 2) {
+        zs[1] = 2 * (nz / 4);
+    } else if (chains == 3) {
+        zs[1] = 2 * ((1 + (nz - 2) / 3 + 1) / 2);
+        zs[2] = 2 * ((1 + 2 * (nz - 2) / 3 + 1) / 2);
+    }
+    int m = 1;
+    for (int j = 1; j < chains; ++j)
+        if (zs[j] >= 2 && zs[j] > zs[m - 1] && zs[j] < nz - 1) zs[m++] = zs[j];
+    for (int j = m; j < 4; ++j) zs[j] = nz - 1;
+    return m;
 }
 
 // order the context stream after all work of the slab driver's other streams (before the state, the
@@ -996,7 +1049,7 @@ void drop_slab(pmc_ctx* c) {
 int slab_join(pmc_ctx* c) {
     pmc_slab* s = c->slab;
     if (!s) return PMC_OK;
-    for (hipStream_t st : {s->aux, s->hi}) {
+    for (hipStream_t st : {s->aux, s->hi[0], s->hi[1]}) {
         if (!st) continue;
         hipError_t e = hipEventRecord(s->ev_b, st);
         if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, s->ev_b, 0);
@@ -1092,6 +1145,25 @@ float* disk_plane(pmc_ctx* c, int z) { return c->disk[c->cur] + (size_t)(z + 1) 
 int16_t* n_plane(pmc_ctx* c, int z) { return c->n[c->cur] + (size_t)(z + 1) * plane_cells(c); }
 
 
+// Strong-scaling rehearsal (PMC_XFER_DELAY_US, microseconds, default 0): after every halo exchange
+// the exchange stream T is held busy for that long by a one-wave spin kernel -- the xGMI time and
+// RCCL latency of a real exchange (3.1 MB each way per run at 128^2 cells per plane), which a
+// one-GPU rehearsal does not pay.  Never set in production runs.
+double xfer_delay_us() {
+    static const double us = [] {
+        const char* v = std::getenv("PMC_XFER_DELAY_US");
+        return v ? std::atof(v) : 0.0;
+    }();
+    return us;
+}
+
+int inject_delay(pmc_slab* s) {
+    const double us = xfer_delay_us();
+    if (us <= 0.0) return PMC_OK;
+    hipError_t e = launch_spin(us, s->aux);
+    return e == hipSuccess ? PMC_OK : hip_fail(e, "injected exchange delay");
+}
+
 // End of a run of colour phases of z parity p (spec v9 groups the 8 phases of a sweep into two
 // runs): during the run only the owned planes of parity p changed, and the one of them another rank
 // holds as a halo is the boundary plane P_p (plane 0 for p = 0, nz-1 for p = 1).  It goes whole
@@ -1107,12 +1179,13 @@ int slab_exchange_run(pmc_ctx* c, int p) {
     const int src = p == 0 ? 0 : nz - 1, dst = p == 0 ? nz : -1;
     if (!s->messages()) {
         PMC_HIP(hipMemcpyAsync(disk_plane(c, dst), disk_plane(c, src), pf * 4, hipMemcpyDeviceToDevice, s->aux));
-        return PMC_OK;
+        return inject_delay(s);
     }
     const int to = p == 0 ? s->below : s->above, from = p == 0 ? s->above : s->below;
     xfer_send(s, disk_plane(c, src), pf * 4, to);
     xfer_recv(s, disk_plane(c, dst), pf * 4, from);
-    return xfer_run(s);
+    if (int rc = xfer_run(s)) return rc;
+    return inject_delay(s);
 }
 
 // both boundary planes with their counts (after shiftCells / initialisation), on aux
@@ -1150,14 +1223,15 @@ int slab_exchange_zplane(pmc_ctx* c, int dir) {
     if (!s->messages()) {
         PMC_HIP(hipMemcpyAsync(disk_plane(c, dst), disk_plane(c, src), pf * 4, hipMemcpyDeviceToDevice, s->aux));
         PMC_HIP(hipMemcpyAsync(n_plane(c, dst), n_plane(c, src), pc * 2, hipMemcpyDeviceToDevice, s->aux));
-        return PMC_OK;
+        return inject_delay(s);
     }
     const int to = dir > 0 ? s->below : s->above, from = dir > 0 ? s->above : s->below;
     xfer_send(s, disk_plane(c, src), pf * 4, to);
     xfer_send(s, n_plane(c, src), pc * 2, to);
     xfer_recv(s, disk_plane(c, dst), pf * 4, from);
     xfer_recv(s, n_plane(c, dst), pc * 2, from);
-    return xfer_run(s);
+    if (int rc = xfer_run(s)) return rc;
+    return inject_delay(s);
 }
 
 }  // namespace
@@ -1207,34 +1281,39 @@ int slab_attach(pmc_ctx* c, int rank, int world, bool messages) {
         drop_slab(c);
         return hip_fail(e, "hipStreamCreate");
     }
-    for (hipEvent_t* ev : {&s->ev_i, &s->ev_b, &s->ev_t, &s->ev_x, &s->ev_run[0][0], &s->ev_run[0][1],
-                           &s->ev_run[1][0], &s->ev_run[1][1], &s->ev_run[2][0], &s->ev_run[2][1]})
+    std::vector<hipEvent_t*> evs = {&s->ev_i, &s->ev_b, &s->ev_t, &s->ev_x};
+    for (hipEvent_t* ev : s->run_events()) evs.push_back(ev);
+    for (hipEvent_t* ev : evs)
         if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) {
             drop_slab(c);
             return hip_fail(e, "hipEventCreate");
         }
-    // Interior planes in two chains (lower and upper part on two streams); PMC_SLAB_CHAINS=1: one
-    // chain (the upper part empty, every interior launch on the context stream)
+    // Interior planes in `chains` chains on as many streams (chain 0 on the context stream);
+    // PMC_SLAB_CHAINS = 1, 2 or 3 (default 2).  With the exchange stream that is at most 4 streams,
+    // the box's GPU_MAX_HW_QUEUES: every chain keeps a hardware queue of its own.
     {
         static const int forced = [] {
             const char* v = std::getenv("PMC_SLAB_CHAINS");
             return v ? std::atoi(v) : 0;
         }();
-        s->chains = forced == 1 ? 1 : 2;
+        s->chains = forced >= 1 && forced <= 3 ? forced : 2;
     }
-    if ((e = hipStreamCreateWithFlags(&s->hi, hipStreamNonBlocking)) != hipSuccess) {
-        drop_slab(c);
-        return hip_fail(e, "hipStreamCreate");
-    }
+    for (int j = 0; j + 1 < s->chains; ++j)
+        if ((e = hipStreamCreateWithFlags(&s->hi[j], hipStreamNonBlocking)) != hipSuccess) {
+            drop_slab(c);
+            return hip_fail(e, "hipStreamCreate");
+        }
     // every "latest" event starts recorded (waits on them are no-ops until real work records them)
-    for (hipEvent_t ev : {s->ev_x, s->ev_run[0][0], s->ev_run[0][1], s->ev_run[1][0], s->ev_run[1][1],
-                          s->ev_run[2][0], s->ev_run[2][1]})
-        if ((e = hipEventRecord(ev, c->stream)) != hipSuccess) {
+    std::vector<hipEvent_t*> latest = {&s->ev_x};
+    for (hipEvent_t* ev : s->run_events()) latest.push_back(ev);
+    for (hipEvent_t* ev : latest)
+        if ((e = hipEventRecord(*ev, c->stream)) != hipSuccess) {
             drop_slab(c);
             return hip_fail(e, "hipEventRecord");
         }
-    // overflow queues of the upper and the boundary chain (they run beside the context stream's)
-    for (int** q : {&c->ovf_aux, &c->ovf_b})
+    // overflow queues of the other interior chains and the boundary chain (they run beside the
+    // context stream's)
+    for (int** q : {&c->ovf_aux, &c->ovf_b, &c->ovf_aux2})
         if (!*q && ((e = hipMalloc(q, c->ovf_bytes)) != hipSuccess ||
                     (e = hipMemsetAsync(*q, 0, c->ovf_bytes, c->stream)) != hipSuccess)) {
             drop_slab(c);
@@ -1323,75 +1402,84 @@ int pmc_slab_exchange(pmc_ctx* c) {
     if (rc) return rc;
     PMC_HIP(hipEventRecord(s->ev_i, c->stream));
     PMC_HIP(hipStreamWaitEvent(s->aux, s->ev_i, 0));
-    PMC_HIP(hipStreamWaitEvent(s->hi, s->ev_i, 0));
+    for (hipStream_t h : s->hi)
+        if (h) PMC_HIP(hipStreamWaitEvent(h, s->ev_i, 0));
     if ((rc = slab_exchange_full(c))) return rc;
     PMC_HIP(hipEventRecord(s->ev_t, s->aux));
     PMC_HIP(hipStreamWaitEvent(c->stream, s->ev_t, 0));
-    PMC_HIP(hipStreamWaitEvent(s->hi, s->ev_t, 0));
-    for (hipEvent_t ev : {s->ev_x, s->ev_run[0][0], s->ev_run[0][1], s->ev_run[1][0], s->ev_run[1][1],
-                          s->ev_run[2][0], s->ev_run[2][1]})
-        PMC_HIP(hipEventRecord(ev, s->aux));
+    for (hipStream_t h : s->hi)
+        if (h) PMC_HIP(hipStreamWaitEvent(h, s->ev_t, 0));
+    PMC_HIP(hipEventRecord(s->ev_x, s->aux));
+    for (hipEvent_t* ev : s->run_events()) PMC_HIP(hipEventRecord(*ev, s->aux));
     return PMC_OK;
 }
 
 int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
     if (!c || !c->slab) return fail(PMC_ERR_ARG, "no slab driver (pmc_slab_init)");
     pmc_slab* s = c->slab;
-    hipStream_t S = c->stream, U = s->hi, T = s->aux;
+    hipStream_t S = c->stream, T = s->aux;
     const int nz = c->P.nz_local;
-    // interior planes [1, nz-1): lower chain L = [1, zs) on S, upper chain U = [zs, nz-1) on its own
-    // stream; zs is even so every parity-q run of L ends at the same side of the split
-    int zs = 2 * (nz / 4);
-    if (s->chains == 1 || zs < 2) zs = nz - 1;                 // one interior chain (or none: nz = 2)
+    // interior planes [1, nz-1) in nc chains: chain j = planes [zs[j], zs[j+1]) on stream ist[j]
+    // (chain 0 on the context stream S); every inner border zs[j] is even, so every parity-q run
+    // of a chain ends at the same side of each border
+    int zs[4];
+    const int nc = slab_split(s->chains, nz, zs);
+    hipStream_t ist[3] = {S, s->hi[0], s->hi[1]};
+    int* iovf[3] = {c->ovf, c->ovf_aux, c->ovf_aux2};
     const pmc_sweep_plan_t plan = pmc_plan_for_sweep_ex(c->P.seed, sweep, c->P.w, c->P.flags);
     int rc;
     // The 8 colour phases form runs of equal z parity q (two runs of 4 with the default plan).  In a
     // run only the planes of parity q change, each reading its own plane and the parity 1-q planes
     // next to it, which no phase of the run writes and no halo of the run changes: every plane's
-    // chain of phases is independent of the other planes' for the whole run.  So each run is three
-    // independent chains of launches:
-    //   L (context stream S): the run's phases on interior planes [1, zs);
-    //   U (second stream):    the run's phases on interior planes [zs, nz-1);
+    // chain of phases is independent of the other planes' for the whole run.  So each run is
+    // nc + 1 independent chains of launches:
+    //   interior chain j (stream ist[j]; j = 0 on the context stream S): the run's phases on the
+    //     interior planes [zs[j], zs[j+1]);
     //   B (exchange stream T): the run's phases on the boundary plane P_q (plane 0 for q = 0, nz-1
     //     for q = 1) -- the only plane of the run that reads a halo (H_{1-q}, received by T at the end
     //     of the previous run) and that another rank holds as a halo -- then the exchange: P_q whole to
     //     the neighbour holding it, H_q from the other side (slab_exchange_run), one message each way.
-    // L's and U's launch gaps and tails overlap each other's work, and the exchange overlaps both.
-    // The chains synchronise only at run boundaries, where a run's reads cross a chain border (with
-    // zs even: q = 1: L's plane 1 reads plane 0 (B's), L's plane zs-1 reads plane zs (U's), B's plane
-    // nz-1 reads plane nz-2 (U's); q = 0: U's plane zs reads plane zs-1 (L's), U's plane nz-2 reads
-    // plane nz-1 (B's), B's plane 0 reads plane 1 (L's)): each waits for the owner chain's previous
-    // run (an event per chain and parity; border_waits derives the set from the plane ownership, so
-    // one interior chain or none works the same way).  Those are also the only readers of the
-    // planes a run overwrites, so the same waits order every overwrite after its readers.  Cells of a colour are independent, so any split of a phase gives the whole-box
-    // result bit for bit (the GPU tests compare every world size with the oracle's whole box).
-    enum { kL = 0, kU = 1, kB = 2 };
+    // The chains' launch gaps and tails overlap each other's work, and the exchange overlaps them.
+    // The chains synchronise only at run boundaries, where a run's reads cross a chain border (the
+    // borders are even: a parity-q plane next to a border reads the plane across it, which the other
+    // chain wrote in its previous run of parity 1-q): each waits for the owner chain's previous run
+    // (an event per chain and parity; border_waits derives the set from the plane ownership, so any
+    // number of interior chains, or none, works the same way).  Those are also the only readers of
+    // the planes a run overwrites, so the same waits order every overwrite after its readers.  Cells
+    // of a colour are independent, so any split of a phase gives the whole-box result bit for bit
+    // (the GPU tests compare every world size and chain count with the oracle's whole box).
+    constexpr int kB = pmc_slab::kB;
     int k = 0;
-    auto phases = [&](hipStream_t st, int* ovf, int z0, int z1, int k0, int k1, int kind) -> int {
+    auto phases = [&](hipStream_t st, int* ovf, int z0, int z1, int k0, int k1, bool boundary) -> int {
         for (int kk = k0; kk < k1; ++kk) {
             int o[3];
             pmc_colour_offset(plan.order[kk], o);
             LaunchTiming lt;
-            hipError_t le = kind == kB
+            hipError_t le = boundary
                 ? launch_subsweep_boundary(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep, c->stats,
                                            ovf, z0, z1, nullptr, 0, st, next_timing(c, 2, &lt))
                 : launch_subsweep(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep, c->stats, ovf, z0,
-                                  z1, st, next_timing(c, 0, &lt));   // both interior chains: kind 0
+                                  z1, st, next_timing(c, 0, &lt));   // every interior chain: kind 0
             if (le != hipSuccess) return hip_fail(le, "subsweep launch");
         }
         return PMC_OK;
     };
     // owner chain of owned plane z; the planes a chain writes in a run of parity q and the other
     // chains owning a plane next to one of them (those it waits for; halos are T's own business)
-    auto owner = [&](int z) { return (z == 0 || z == nz - 1) ? (int)kB : (z < zs ? (int)kL : (int)kU); };
+    auto owner = [&](int z) {
+        if (z == 0 || z == nz - 1) return kB;
+        int j = 0;
+        while (j + 1 < nc && z >= zs[j + 1]) ++j;
+        return j;
+    };
     auto border_waits = [&](int chain, int z0, int z1, int q, hipStream_t st, int parity) -> int {
-        bool need[3] = {false, false, false};
+        bool need[4] = {false, false, false, false};
         for (int z = z0; z < z1; ++z) {
             if ((z & 1) != q) continue;
             for (int zn : {z - 1, z + 1})
                 if (zn >= 0 && zn < nz && owner(zn) != chain) need[owner(zn)] = true;
         }
-        for (int j = 0; j < 3; ++j)
+        for (int j = 0; j < 4; ++j)
             if (need[j]) PMC_HIP(hipStreamWaitEvent(st, s->ev_run[j][parity], 0));
         return PMC_OK;
     };
@@ -1401,31 +1489,22 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
         while (k1 < 8 && plan.order[k1] % 2 == q) ++k1;           // run [k, k1)
         const int p = 1 - q;                                      // parity of the previous run
         // the sweep's first run needs no border waits: the previous sweep's shift joined every
-        // chain, and U and T wait for it (a stream wait costs a barrier packet on the critical path)
+        // chain, and the other streams wait for it (a stream wait costs a barrier packet on the
+        // critical path)
         const bool first = k == 0;
-        // L
-        if (!first && (rc = border_waits(kL, 1, zs, q, S, p))) return rc;
-        if (zs > 1 && (rc = phases(S, c->ovf, 1, zs, k, k1, kL))) return rc;
-        PMC_HIP(hipEventRecord(s->ev_run[kL][q], S));
-        // U
-        if (!first && (rc = border_waits(kU, zs, nz - 1, q, U, p))) return rc;
-        if (nz - 1 > zs && (rc = phases(U, c->ovf_aux, zs, nz - 1, k, k1, kU))) return rc;
-        PMC_HIP(hipEventRecord(s->ev_run[kU][q], U));
+        for (int j = 0; j < nc; ++j) {
+            if (!first && (rc = border_waits(j, zs[j], zs[j + 1], q, ist[j], p))) return rc;
+            if (zs[j + 1] > zs[j] && (rc = phases(ist[j], iovf[j], zs[j], zs[j + 1], k, k1, false))) return rc;
+            PMC_HIP(hipEventRecord(s->ev_run[j][q], ist[j]));
+        }
         // B, then the exchange
         const int zb = q == 0 ? 0 : nz - 1;
         if (!first && (rc = border_waits(kB, zb, zb + 1, q, T, p))) return rc;
-        if ((rc = phases(T, c->ovf_b, zb, zb + 1, k, k1, kB))) return rc;
+        if ((rc = phases(T, c->ovf_b, zb, zb + 1, k, k1, true))) return rc;
         PMC_HIP(hipEventRecord(s->ev_run[kB][q], T));
         if ((rc = slab_exchange_run(c, q))) return rc;
         k = k1;
     }
-    // shiftCells reads every plane and both halos: join U and T into S.  (Splitting the shift over
-    // the three chains measured slower: the boundary chain, whose small launches wait for the
-    // interior chains' waves, is the last to finish a sweep, and its share of the shift came after.)
-    PMC_HIP(hipEventRecord(s->ev_b, U));
-    PMC_HIP(hipStreamWaitEvent(S, s->ev_b, 0));
-    PMC_HIP(hipEventRecord(s->ev_x, T));
-    PMC_HIP(hipStreamWaitEvent(S, s->ev_x, 0));
     // after the 8 phases both halo planes are exact copies of the neighbours' planes, so
     // every halo plane whose new content depends only on planes this rank holds is shifted here,
     // bit-identical to its owner's result.  Along x or y that is both halo planes (no exchange at
@@ -1433,19 +1512,60 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
     // plane next to it), and the other one is received: one plane with its counts, one direction.
     int zl0, zl1;
     const int dir = slab_shift_planes(nz, plan, &zl0, &zl1);
+    // Split shift (PMC_SLAB_SPLIT_SHIFT=1, shifts along x or y): of all the shift's output planes
+    // only the halo H_q the LAST run's exchange fills reads that exchange (along x/y an output plane
+    // reads only itself).  The context stream S shifts every other plane as soon as the interior
+    // chains and the boundary chain's last phases are done -- not waiting for the exchange -- and T
+    // shifts H_q after it: the exchange leaves the sweep's critical path (it matters once the
+    // exchange takes xGMI time: PMC_XFER_DELAY_US rehearsals).  The next sweep's interior chains
+    // read no halo; T, which runs the next boundary phases, is in order after its own part.
+    static const bool split_env = [] {
+        const char* v = std::getenv("PMC_SLAB_SPLIT_SHIFT");
+        return v && std::atoi(v) == 1;
+    }();
+    const int q_last = plan.order[7] % 2;
+    const int hq = q_last == 0 ? nz : -1;                    // the halo the last exchange fills
+    const bool split = split_env && plan.f != 2 && hq >= zl0 && hq < zl1;
+    for (int j = 1; j < nc; ++j) {
+        PMC_HIP(hipEventRecord(s->ev_b, ist[j]));
+        PMC_HIP(hipStreamWaitEvent(S, s->ev_b, 0));
+    }
     LaunchTiming lts;
-    hipError_t e = launch_shift_planes(c->G, c->disk[c->cur], c->n[c->cur], c->disk[c->cur ^ 1], c->n[c->cur ^ 1],
-                                       plan.f, plan.d, c->flags, zl0, zl1, S, next_timing(c, 1, &lts));
-    if (e != hipSuccess) return hip_fail(e, "shift launch");
+    hipError_t e;
+    if (split) {
+        // S after B's last phases (ev_run[kB][q_last]: recorded on T after every earlier exchange)
+        PMC_HIP(hipStreamWaitEvent(S, s->ev_run[kB][q_last], 0));
+        const int a0 = hq == -1 ? 0 : zl0, a1 = hq == -1 ? zl1 : nz;
+        e = launch_shift_planes(c->G, c->disk[c->cur], c->n[c->cur], c->disk[c->cur ^ 1], c->n[c->cur ^ 1], plan.f,
+                                plan.d, c->flags, a0, a1, S, next_timing(c, 1, &lts));
+        if (e != hipSuccess) return hip_fail(e, "shift launch");
+        e = launch_shift_planes(c->G, c->disk[c->cur], c->n[c->cur], c->disk[c->cur ^ 1], c->n[c->cur ^ 1], plan.f,
+                                plan.d, c->flags, hq, hq + 1, T, nullptr);
+        if (e != hipSuccess) return hip_fail(e, "shift launch (halo)");
+    } else {
+        // shiftCells reads every plane and both halos: the other chains and T joined into S
+        PMC_HIP(hipEventRecord(s->ev_x, T));
+        PMC_HIP(hipStreamWaitEvent(S, s->ev_x, 0));
+        e = launch_shift_planes(c->G, c->disk[c->cur], c->n[c->cur], c->disk[c->cur ^ 1], c->n[c->cur ^ 1], plan.f,
+                                plan.d, c->flags, zl0, zl1, S, next_timing(c, 1, &lts));
+        if (e != hipSuccess) return hip_fail(e, "shift launch");
+    }
     c->cur ^= 1;
-    // U and T continue after the shift (it rewrote every plane); the z halo arrives on T, overlapping
-    // the next sweep's first interior launches (they read no halo).  The next sweep's first run
-    // waits for nothing else (no border waits), so no "previous run" event is recorded here.
+    // the other chains and T continue after the shift (it rewrote every plane); the z halo arrives
+    // on T, overlapping the next sweep's first interior launches (they read no halo).  The next
+    // sweep's first run waits for nothing else (no border waits), so no "previous run" event is
+    // recorded here.
     PMC_HIP(hipEventRecord(s->ev_i, S));
-    PMC_HIP(hipStreamWaitEvent(U, s->ev_i, 0));
+    for (int j = 1; j < nc; ++j) PMC_HIP(hipStreamWaitEvent(ist[j], s->ev_i, 0));
     PMC_HIP(hipStreamWaitEvent(T, s->ev_i, 0));
     if (dir != 0 && (rc = slab_exchange_zplane(c, dir))) return rc;
     PMC_HIP(hipEventRecord(s->ev_x, T));
+    return PMC_OK;
+}
+
+int pmc_slab_layout(pmc_ctx* c, int* n_chains, int borders[4]) {
+    if (!c || !c->slab || !n_chains || !borders) return fail(PMC_ERR_ARG, "no slab driver (pmc_slab_init)");
+    *n_chains = slab_split(c->slab->chains, c->P.nz_local, borders);
     return PMC_OK;
 }
 
@@ -1510,7 +1630,9 @@ int pmc_timing_kinds(pmc_ctx* c, int enable, double ms[3], int count[3]) {
     if (!c->tkind.empty()) {
         PMC_HIP(hipStreamSynchronize(c->stream));
         if (c->slab) PMC_HIP(hipStreamSynchronize(c->slab->aux));
-        if (c->slab && c->slab->hi) PMC_HIP(hipStreamSynchronize(c->slab->hi));
+        if (c->slab)
+            for (hipStream_t h : c->slab->hi)
+                if (h) PMC_HIP(hipStreamSynchronize(h));
         for (size_t k = 0; k < c->tkind.size(); ++k) {
             float t = 0.0f;
             PMC_HIP(hipEventElapsedTime(&t, c->tev[2 * k], c->tev[2 * k + 1]));

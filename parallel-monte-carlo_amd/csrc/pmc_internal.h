@@ -39,6 +39,7 @@ constexpr int kStatCounters = 4;    // de_fixed, accepted, trials, evaluated
 __host__ __device__ constexpr int stat_index(int counter, int slot) {
     return PMC_STATS_LANES ? slot * kStatCounters + counter : counter * kStatSlots + slot;
 }
+constexpr int kSmallSweeps = 32;   // k_sweep_small: sweep plans per launch (pmc_run_small checks each launch)
 constexpr int kOvfHead = 2;        // ints of the subsweep overflow-queue header (pmc_kernels.hip)
 
 // Unsigned division by an invariant d: n / d = (hi + ((n - hi) >> sh1)) >> sh2, hi = umulhi(n, mul)
@@ -114,6 +115,8 @@ hipError_t launch_energy(const DevGeom& g, const float* disk, const int16_t* n,
 // the cells of one colour of one plane: mode 0 plane -> packed buffer, 1 packed -> plane,
 // 2 plane -> plane; (cps_x/2)*(cps_y/2)*3*nmax floats
 hipError_t launch_colour_rows(const DevGeom& g, const float* src, float* dst, int colour, int mode, hipStream_t st);
+// rehearsal only: a one-wave kernel that occupies `st` for `us` microseconds (injected exchange delay)
+hipError_t launch_spin(double us, hipStream_t st);
 hipError_t launch_selftest(const uint32_t* words, int count, float* out_f, double* out_d,
                            float rc2, hipStream_t st);
 

@@ -1113,9 +1113,8 @@ static int64_t env_cells(const char* name, int64_t dflt) {
 // blocks on XCD 0 (a dispatch that is not round-robin) flags error bit 4.  Every cell
 // visit uses the full-capacity LDS layout (27*nmax partners: no overflow queue), 9.9 KB per wave,
 // 16 waves per CU: XCD 0 holds 512 participants.  Barrier waits give up after ~1 s of s_memrealtime
-// (error bit 8) so a participant that never arrives cannot hang the GPU.
+// (error flag value 8, bit 3) so a participant that never arrives cannot hang the GPU.
 // ------------------------------------------------------------------------------------------
-constexpr int kSmallSweeps = 32;   // sweep plans per launch
 struct SmallPlans {
     int n;                          // sweeps in this launch
     uint32_t first;                 // sweep index of the first
@@ -1148,7 +1147,7 @@ __device__ __forceinline__ bool small_barrier(unsigned* bar, unsigned target, ui
 }
 
 // shiftCells of cells [c0, c0 + 64/NSLOT) (one cell per NSLOT-lane group), the arithmetic of k_shift
-// (shiftCells.h:46-108, float s of the fixed copy) for one cell per lane group
+// (VS shiftCells.h:38-108, float s of the fixed copy) for one cell per lane group
 template <int NSLOT>
 __device__ __forceinline__ void shift_cells_wave(const DevGeom& g, const float* __restrict__ din,
                                                  const int16_t* __restrict__ nin, float* __restrict__ dout,
@@ -1299,7 +1298,7 @@ __global__ __launch_bounds__(kShiftThreads) void k_shift(DevGeom g, const float*
     const float w = g.w;
     const int cps_f = f == 0 ? g.cps_x : (f == 1 ? g.cps_y : g.cps_z);
     const float Lf = f == 0 ? g.Lx : (f == 1 ? g.Ly : g.Lz);
-    const int dir = (d <= 0) ? -1 : 1;                     // shiftCells.h:46-53
+    const int dir = (d <= 0) ? -1 : 1;                     // VS shiftCells.h:38-44
     const float s = w * (float)dir;
     const uint32_t plane = (uint32_t)g.cps_x * (uint32_t)g.cps_y;
     const int pp = p < nm ? p : 0;
@@ -1318,7 +1317,7 @@ __global__ __launch_bounds__(kShiftThreads) void k_shift(DevGeom g, const float*
         const int xx = live[j] ? x : 0;
         int cidf = f == 0 ? xx : (f == 1 ? y : g.z0 + zl);
         if (cidf < 0) cidf += cps_f; else if (cidf >= cps_f) cidf -= cps_f;   // halo planes wrap
-        offset[j] = (float)cidf * w - Lf / 2.0f;           // :55
+        offset[j] = (float)cidf * w - Lf / 2.0f;           // VS :46
         int nbg = cidf + dir;
         if (nbg < 0) nbg = cps_f - 1; else if (nbg >= cps_f) nbg = 0;
         int nx = xx, ny = y, nz = zl;
@@ -1381,7 +1380,7 @@ __global__ __launch_bounds__(kShiftThreads) void k_shift(DevGeom g, const float*
             if (dst < nm) {
 #pragma unroll
                 for (int dim = 0; dim < 3; ++dim)
-                    dout[ob + (uint64_t)(dim * nm + dst)] = (dim == f) ? ((Dn + offset[j]) + s) : nbv[j][dim];   // own offset (shiftCells.h:100)
+                    dout[ob + (uint64_t)(dim * nm + dst)] = (dim == f) ? ((Dn + offset[j]) + s) : nbv[j][dim];   // own offset (VS shiftCells.h:96)
             }
         }
         if (live[j] && p == 0) {
@@ -1627,7 +1626,11 @@ constexpr int kESeg = PMC_ENERGY_SEG;
 constexpr int kERows = 5;                   // the rows of an interior cell's half shell
 constexpr int kEStaged = kERows * (kESeg + 2);   // staged cells per segment (< 64: one lane each)
 static_assert(kEStaged < 64, "one lane per staged cell");
-constexpr int kECap = kESeg == 6 ? 288 : 384;   // staged particles
+// staged particles per segment: 288 at 6-cell segments with the 128-entry ring (the 5 KiB budget
+// below; the near-lattice start of the configs peaks at 281 per segment, so a box a few percent
+// denser than 4.77 per cell queues some segments for MODE 2), 240 with PMC_ENERGY_STEP=2's 256-entry
+// ring, 384 at 8-cell segments (6.5 KiB)
+constexpr int kECap = kESeg == 6 ? (kEnergyRing == 128 ? 288 : 240) : 384;
 constexpr int kEList = 14 * 16;             // a cell's filtered partner list (indices into the staging)
 #ifndef PMC_ENERGY_OWN_LDS
 #define PMC_ENERGY_OWN_LDS 1   // pair loop: own particle from LDS (1) or by v_readlane (0)
@@ -2175,7 +2178,22 @@ __global__ void k_selftest(const uint32_t* __restrict__ words, int count, float*
     out_d[2 * i + 1] = (double)pmc_to_fixed((double)out_f[4 * i + 3]);
 }
 
+// Strong-scaling rehearsal only (PMC_XFER_DELAY_US): one wave that keeps the exchange stream busy
+// for `ticks` of the 100 MHz real-time counter after a halo exchange -- the xGMI transfer time and
+// RCCL latency a one-GPU rehearsal does not see.  Bounded by the tick count (no memory access).
+__global__ void k_spin(uint64_t ticks) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
 }  // namespace
+
+hipError_t launch_spin(double us, hipStream_t st) {
+    const uint64_t ticks = us > 0.0 ? (uint64_t)(us * 100.0) : 0;   // s_memrealtime: 100 MHz
+    if (ticks > 100000000ull) return hipErrorInvalidValue;          // at most 1 s
+    hipLaunchKernelGGL(k_spin, dim3(1), dim3(kWave), 0, st, ticks);
+    return hipGetLastError();
+}
 
 // ------------------------------------------------------------------------------------------
 // launchers
@@ -2464,17 +2482,25 @@ hipError_t launch_energy(const DevGeom& g, const float* disk, const int16_t* n,
                            (int64_t)(g.nz_local - 2) * (2 * (int64_t)g.cps_x + 2 * (int64_t)(g.cps_y - 2));
     const size_t lds_rows = sizeof(float) * (3 * kECap + kEnergyRing) + sizeof(uint16_t) * kEList + sizeof(int2) * 64;
     static_assert(sizeof(float) * (3 * kECap + kEnergyRing) + sizeof(uint16_t) * kEList + sizeof(int2) * 64 <= 5120 || kESeg != 6,
-                  "energy rows: 8 waves per SIMD");
+                  "energy rows: 8 waves per SIMD");   // (holds for both ring sizes, kECap above)
     const dim3 grid_rows((unsigned)energy_segments(g));
+    // The rows kernel stages a cell's half-shell partner list of at most kEList entries: with nmax >
+    // 16 it could overflow, and every segment would be queued for MODE 2 -- run the per-cell kernel
+    // over every cell instead (MODE 0, ~total/16 waves).  MODE 2's grid covers the queue's worst case
+    // up to the chip's wave slots (blocks past the queue length exit at once): a dense box that
+    // queues many segments keeps the whole chip (a fixed 64-wave grid was ~100x slower then).
+    const bool per_cell = legacy || 14 * g.nmax > kEList;
+    const unsigned seg_total = (unsigned)energy_segments(g);
+    const dim3 grid_q(seg_total < 8192u ? (seg_total > 0u ? seg_total : 1u) : 8192u);
     auto go = [&](auto k0, auto k1, auto k2, auto kr) {
-        if (legacy) {
+        if (per_cell) {
             hipLaunchKernelGGL(k0, grid, block, lds, st, g, disk, n, acc, tc, segq, div_nsx);
             return;
         }
         hipLaunchKernelGGL(kr, grid_rows, block, lds_rows, st, g, disk, n, acc, segq, div_nsx, div_cy, cap);
         hipLaunchKernelGGL(k1, dim3((unsigned)((n_edge + kEdgeCells - 1) / kEdgeCells)), block, lds, st, g, disk, n,
                            acc, (uint32_t)n_edge, segq, div_nsx);
-        hipLaunchKernelGGL(k2, dim3(64), block, lds, st, g, disk, n, acc, tc, segq, div_nsx);
+        hipLaunchKernelGGL(k2, grid_q, block, lds, st, g, disk, n, acc, tc, segq, div_nsx);
     };
 #define PMC_ENERGY_GO(NS, O32) go(k_energy<NS, O32, 0>, k_energy<NS, O32, 1>, k_energy<NS, O32, 2>, k_energy_rows<NS, O32>)
     switch (g.nslot) {

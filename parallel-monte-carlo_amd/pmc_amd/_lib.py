@@ -118,6 +118,7 @@ def lib():
         _sig(L, "pmc_slab_exchange", i32, _vp)
         _sig(L, "pmc_slab_sweep", i32, _vp, u32)
         _sig(L, "pmc_slab_finish", i32, _vp)
+        _sig(L, "pmc_slab_layout", i32, _vp, _vp, _vp)
         _sig(L, "pmc_slab_observables", i32, _vp, i32, C.POINTER(Stats), C.POINTER(C.c_double))
         _sig(L, "pmc_slab_timing", i32, _vp, i32, _vp, _vp, _vp, _vp)
         _sig(L, "pmc_timing", i32, _vp, i32, _vp, _vp, _vp, _vp)

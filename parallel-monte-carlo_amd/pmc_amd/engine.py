@@ -180,6 +180,13 @@ class PmcContext:
     def slab_sweep(self, s: int) -> None:
         check("pmc_slab_sweep", lib().pmc_slab_sweep(self._h, s))
 
+    def slab_layout(self) -> list:
+        """The interior chains of pmc_slab_sweep as (first plane, end plane) pairs."""
+        n = C.c_int(0)
+        b = (C.c_int * 4)()
+        check("pmc_slab_layout", lib().pmc_slab_layout(self._h, C.byref(n), b))
+        return [(b[j], b[j + 1]) for j in range(n.value)]
+
     def slab_finish(self) -> None:
         check("pmc_slab_finish", lib().pmc_slab_finish(self._h))
 

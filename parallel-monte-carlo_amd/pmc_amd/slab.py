@@ -398,10 +398,13 @@ def _rccl_lib_path() -> Optional[str]:
 class SlabDriver:
     """The product multi-GPU path: the C slab driver (pmc_slab_*), one process per GPU.
 
-    The sweep schedule (interior on the context stream, each colour's boundary plane on an
-    auxiliary stream beside it, colour-packed RCCL send/recv of the boundary cells) runs in C, so
-    the host issues a sweep in a few dozen HIP/RCCL calls.  SlabSimulation above is the same
-    schedule in Python over torch.distributed; the CPU tests drive it with the oracle and gloo.
+    The sweep schedule runs in C (pmc_slab_sweep): the 8 colour phases form two
+    runs of equal z parity; per run the interior planes go in 1-3 launch chains on their own streams
+    (PMC_SLAB_CHAINS) and the run's boundary plane on the exchange stream, which then sends that whole
+    plane to the neighbour holding it as a halo and receives the opposite halo (one RCCL send/recv
+    each way per run); after shiftCells only a z shift needs one more plane.  The host issues a sweep
+    in a few dozen HIP/RCCL calls.  SlabSimulation above is the older per-colour schedule in Python
+    over torch.distributed; the CPU tests drive it with the oracle and gloo.
     """
 
     def __init__(self, cps: int, nz_local: int, rank: int, world: int, stream=None, atoms_per_rank: int = 0,

@@ -185,10 +185,20 @@ def test_local_group_missing_rank_fails_not_hangs(pmc):
     group.close()
 
 
-def test_c_slab_driver_one_chain_world4(pmc, oracle):
-    """PMC_SLAB_CHAINS=1 (one plane chain per rank: every phase one launch on the context stream),
-    world 4 through the in-process transport, equals the oracle's whole box.  Subprocess: the
-    switch is read once per process."""
+@pytest.mark.parametrize("chains,split,world,cps,nz,atoms", [
+    (1, 0, 4, 16, 4, 10_000),
+    (3, 0, 2, 32, 16, 120_000),     # interior chains [1,6), [6,10), [10,15)
+    (3, 0, 4, 32, 8, 120_000),      # [1,4), [4,6), [6,7)
+    (2, 1, 4, 32, 8, 120_000),      # split shift: the last exchange's halo shifted on T
+    (3, 1, 2, 32, 16, 120_000),
+])
+def test_c_slab_driver_chain_count(pmc, oracle, chains, split, world, cps, nz, atoms):
+    """PMC_SLAB_CHAINS=1 (one interior chain per rank: every phase one launch on the context
+    stream) and =3 (three interior chains on three streams beside the exchange stream), and
+    PMC_SLAB_SPLIT_SHIFT=1 (x/y shifts: the halo the last exchange fills shifted on the exchange
+    stream, every other plane on the context stream without waiting for that exchange), through the
+    in-process transport, equal the oracle's whole box over 8 sweeps with shifts along x, y and z
+    both ways.  Subprocess: the switches are read once per process."""
     import subprocess
     import sys
     code = r'''
@@ -198,7 +208,7 @@ import pmc_amd, pmc_oracle
 from test_gpu_multirank import _run_ranks, _window
 from pmc_amd.engine import LocalGroup
 from pmc_amd.slab import SlabDriver
-world, cps, nz, atoms = 4, 16, 4, 10000
+world, cps, nz, atoms, chains = (int(v) for v in sys.argv[4:9])
 first = _window(pmc_oracle, 8)
 pmc_amd.lib()
 g = LocalGroup(world)
@@ -206,15 +216,17 @@ keep = []
 def main(r):
     d = SlabDriver(cps=cps, nz_local=nz, rank=r, world=world, atoms_total=atoms, local_group=g)
     keep.append(d)
+    lay = d.ctx.slab_layout()
     d.run(first, 8)
-    return d.owned(), d.ctx.stats()
+    return d.owned(), d.ctx.stats(), lay
 res = _run_ranks(world, main)
-st = pmc_oracle.OracleState(pmc_oracle.make_params(cps=cps))
+st = pmc_oracle.OracleState(pmc_oracle.make_params(cps=cps, cps_z=world * nz))
 st.init_lattice(atoms)
 st.run(first, 8)
 plane, row = cps * cps, 48
 tot = {}
-for r, ((d, n), s) in enumerate(res):
+for r, ((d, n), s, lay) in enumerate(res):
+    assert len(lay) == chains and lay[0][0] == 1 and lay[-1][1] == nz - 1, lay
     ref = slice(r * nz * plane, (r + 1) * nz * plane)
     assert np.array_equal(n, st.n[ref])
     assert pmc_oracle.valid_slots_equal(d, n, st.disk[ref.start * row:ref.stop * row], st.n[ref], 16)
@@ -225,8 +237,11 @@ print("ok")
 '''
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = subprocess.run([sys.executable, "-c", code, os.path.join(repo, "parallel-monte-carlo_amd"),
-                          os.path.join(repo, "oracle"), os.path.join(repo, "tests")],
-                         env=dict(os.environ, PMC_SLAB_CHAINS="1"), capture_output=True, text=True, timeout=300)
+                          os.path.join(repo, "oracle"), os.path.join(repo, "tests"),
+                          str(world), str(cps), str(nz), str(atoms), str(chains)],
+                         env=dict(os.environ, PMC_SLAB_CHAINS=str(chains), PMC_SLAB_SPLIT_SHIFT=str(split)),
+                         capture_output=True, text=True,
+                         timeout=300)
     assert out.returncode == 0, out.stderr[-3000:]
     assert "ok" in out.stdout
 
@@ -300,3 +315,67 @@ def test_config5_world8_256_equals_oracle(pmc, oracle):
     assert {(f, d > 0) for _, f, d in plans} == {(2, True), (2, False)}
     _world_vs_oracle(pmc, oracle, world=8, cps=256, nz=32, atoms=80_000_000, first=13, count=2,
                      lattice_cps_z=256)
+
+
+def test_bench_parity_leg_slab_world4(pmc, oracle):
+    """bench.py's N > 1 parity leg (parity_leg_slab) at world 4 on one GPU: four slab ranks in
+    threads over the in-process transport, a thread-level gather standing in for dist.gather.
+    Every rank restores its timed-start storage, reruns the sample's sweep through the slab driver
+    and contributes to pmc_slab_observables; rank 0 compares the gathered whole box with the oracle's
+    sweep from the same state: every occupied slot, the four counters, the energy (kernel.cu:452-470),
+    all exact.  This is the collective rerun and observables path the driver's SCALE line uses."""
+    import sys
+    import threading
+    from pmc_amd.engine import LocalGroup
+    from pmc_amd.slab import SlabDriver
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, repo)
+    import bench
+    world, cps, nz, atoms, first = 4, 32, 8, 120_000, 5
+    plane, row = cps * cps, 3 * 16
+    pmc.lib()
+    group = LocalGroup(world)
+    bar = threading.Barrier(world, timeout=120)
+    parts = [None] * world
+    whole_box = {}
+
+    def make_thread_gather(rank):
+        def gather(disk_s, n_s):
+            parts[rank] = (disk_s[plane * row:(nz + 1) * plane * row].copy(), n_s[plane:(nz + 1) * plane].copy())
+            bar.wait()
+            out = None
+            if rank == 0:
+                out = (np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts]))
+            bar.wait()
+            return out
+        return gather
+
+    drivers = [None] * world
+
+    def rank_main(r):
+        d = SlabDriver(cps=cps, nz_local=nz, rank=r, world=world, atoms_total=atoms, local_group=group)
+        drivers[r] = d
+        d.run(0, first)                                 # warm-up sweeps 0..first-1
+        d.ctx.synchronize()
+        disk_s, n_s = d.ctx.copy_out()                  # the timed region's start state (storage)
+        gather = make_thread_gather(r)
+        whole = gather(disk_s, n_s)
+        if r == 0:                                      # the oracle's sample sweep on the whole box
+            st = oracle.OracleState(oracle.make_params(cps=cps, cps_z=world * nz))
+            st.disk[:] = whole[0]
+            st.n[:] = whole[1]
+            assert st.run(first, 1) == 0
+            whole_box["ost"] = st
+        bar.wait()
+        return bench.parity_leg_slab(d.ctx, d.sweep, d.finish, disk_s, n_s, first, 0.0, gather,
+                                     whole_box.get("ost"), r)
+
+    res = _run_ranks(world, rank_main, timeout=300)
+    for d in drivers:
+        d.ctx.close()
+    group.close()
+    assert all(v is None for v in res[1:])
+    rec = res[0]
+    assert rec["state_bitwise_equal"] is True
+    assert rec["counters_equal"] is True
+    assert rec["energy_rel_err"] == 0.0 and rec["acceptance_rel_err"] == 0.0

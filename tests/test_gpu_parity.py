@@ -241,7 +241,8 @@ def test_graph_replay_equals_oracle(pmc, oracle):
 def test_small_box_persistent_equals_oracle(pmc, oracle, cps, atoms):
     """pmc_run_small (whole sweeps in one launch on XCD 0, in-kernel barriers) equals the oracle bit
     for bit over 40 sweeps (two launches of 32 + 8), 512 participants looping over up to 4 cells per
-    colour phase at 24^3; pmc_start takes the same path for these boxes."""
+    colour phase at 24^3.  (pmc_start does not take this path by default -- the eager
+    one-launch-per-phase sweep is faster at every size -- only with PMC_SMALL=1.)"""
     cx, cy, cz = cps
     ctx = _ctx(pmc, cx, cps_y=cy, cps_z=cz)
     ctx.init_lattice(atoms)
@@ -397,6 +398,34 @@ print("ok")
                          capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-3000:]
     assert "ok" in out.stdout
+
+
+def test_energy_nmax32_and_dense_box_fast(oracle, pmc):
+    """the energy's row-segment kernel cannot stage a cell's partner list at nmax > 16,
+    and a box denser than the configs' 4.77 per cell overflows its staging capacity.  Both go to
+    per-cell kernels that keep the whole chip busy (nmax 32: every cell per cell, MODE 0; over-full
+    segments: the MODE-2 queue over up to 8192 waves): bitwise equal to orc_energy and fast -- a
+    48^3 box at nmax 32 and a 48^3 box at 7.5 particles per cell (whose near-lattice segments
+    overflow the staging) each under 2 ms per call, ~20x the expected time (the fixed 64-wave queue grid of round 3
+    took ~100x the per-cell time)."""
+    import time
+    for nmax, atoms in ((32, 530_000), (16, 830_000)):
+        ctx = pmc.PmcContext(48, nmax=nmax)
+        ctx.init_lattice(atoms)
+        ctx.energy()                      # warm-up (first launch of each kernel)
+        t0 = time.perf_counter()
+        for _ in range(5):
+            e = ctx.energy()
+        dt = (time.perf_counter() - t0) / 5
+        disk, n = ctx.copy_out()
+        st = oracle.OracleState(oracle.make_params(cps=48, nmax=nmax))
+        st.disk[:] = disk
+        st.n[:] = n
+        oracle.set_threads(8)
+        assert e == st.energy(), (nmax, e, st.energy())
+        oracle.set_threads(0)
+        assert dt < 0.002, (nmax, atoms, dt)
+        ctx.close()
 
 
 @pytest.mark.parametrize("rccl", [False, True])
