@@ -38,6 +38,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "parallel-monte-carlo_amd"))
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+FP32_PEAK_TFLOPS = 157.3   # MI355X vector FP32 (no MFMA on this path)
 
 CONFIG_NAMES = {
     "2": "BASELINE config 2: 64^3 cells, 1e6 particles, 1 MI355X, single-colour sweep (a step is one colour "
@@ -291,9 +292,22 @@ def traffic_from_profile(config: str, slab: bool, nz_local: int) -> dict | None:
     except Exception:
         return None
     if not slab:
-        return t
+        # the top level is the config-3 whole box (128^3/1e7); other whole boxes under "box"
+        return t if config == "3" else (t.get("box") or {}).get(config)
     return (t.get("slab") or {}).get(f"{config}:{nz_local}")
 
+
+
+def valu_from_profile() -> dict | None:
+    """The dominant kernel's VALU-issue roof from its committed SQ counters (profiles/pmc_valu.json,
+    tools/valu_roof.py): issue cycles per SIMD at the measured per-class costs against the launch's
+    cycles -- the roof that binds this kernel."""
+    path = os.path.join(REPO, "profiles", "pmc_valu.json")
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except Exception:
+        return None
 
 
 def _hip_d2d(dst: int, src: int, nbytes: int, stream: int) -> None:
@@ -498,7 +512,9 @@ def main() -> int:
                      for a, b in chains]
         sub_launch_bytes = sum(per_chain) / len(per_chain) if per_chain else 0.0
         roof_kernel = ("k_subsweep<16,16,true> (a slab colour phase's interior launches, planes "
-                       + " and ".join(f"[{a},{b})" for a, b in chains) + ", mean bytes per launch)")
+                       + " and ".join(f"[{a},{b})" for a, b in chains) + ", mean bytes per launch; "
+                       "per CHAIN: the chains run concurrently and share HBM, so achieved/frac describe "
+                       "one chain's launch, not the chip's rate)")
     e_start = sim.energy()      # cell-list energy of the state the timed region starts from
     # The host analysis above leaves the GPU idle, and an idle MI355X comes back at a lower clock:
     # after a 0.5 s gap the first sweeps take 3.0-3.3 ms and the rate settles at 2.53 ms only
@@ -562,6 +578,25 @@ def main() -> int:
         avg_launch_s = (tm["subsweep_ms"] / n_launch * 1e-3) if n_launch else None
         achieved = (sub_launch_bytes / avg_launch_s / 1e9) if avg_launch_s else None
         traffic = traffic_from_profile(config, slab, nz_local)
+        # FP32 work of the moves (14 FLOP per pair evaluation, old + new position,
+        # against the S_c - 1 stencil partners of each evaluated move; the mean stencil of the
+        # visited cells stands for each cell's) per launch, over the HIP-event launch time
+        fp32 = None
+        if avg_launch_s and not slab:
+            ne = n_owned > 0
+            s_mean = float(stencil[ne].mean()) if ne.any() else 0.0
+            launches = args.steps * (1 if config == "2" else 8)
+            flop = 28.0 * st["evaluated"] / launches * max(s_mean - 1.0, 0.0)
+            fp32 = {"achieved": flop / avg_launch_s / 1e12, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": flop / avg_launch_s / 1e12 / FP32_PEAK_TFLOPS, "flop_per_launch": flop,
+                    "model": "28 FLOP x (mean stencil - 1) per evaluated move (SURVEY.md 8d)"}
+        valu = valu_from_profile() if config == "3" else None   # profiled on the config-3 launch
+        shift_bytes = None
+        if tm["n_shift"]:
+            # shiftCells (VS shiftCells.h:23-112): per output cell, read its own occupied slots and
+            # those of its dir-neighbour with both counts, write the new occupied slots and count --
+            # 12 B per particle read twice (own and as a neighbour) and written once, 6 B of counts
+            shift_bytes = float(36 * int(n_owned.sum()) + 6 * n_owned.size)
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                 "traffic": traffic.get("subsweep_bytes_per_launch") if traffic else None,
@@ -570,6 +605,16 @@ def main() -> int:
                 "launch_ms": avg_launch_s * 1e3 if avg_launch_s else None,
                 "launches_timed": n_launch,
                 "shift_ms": tm["shift_ms"] / tm["n_shift"] if tm["n_shift"] else None,
+                "shift": ({"algorithmic_bytes_per_launch": shift_bytes,
+                           "achieved": shift_bytes / (tm["shift_ms"] / tm["n_shift"] * 1e-3) / 1e9,
+                           "frac": shift_bytes / (tm["shift_ms"] / tm["n_shift"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                           "model": "36 B per particle + 6 B per cell (own + neighbour occupied slots read, "
+                                    "new slots written, counts)"}
+                          if shift_bytes and tm["n_shift"] and tm["shift_ms"] > 0 else None),
+                "fp32": fp32,
+                "valu": valu,
+                "binding": ("valu-issue (roofline.valu.frac; HBM frac and fp32 frac are far below it)"
+                            if valu else None),
                 "boundary_launch_ms": tm["boundary_ms"] / tm["n_boundary"] if tm["n_boundary"] else None,
                 "algorithmic_bytes_per_launch": sub_launch_bytes}
     # CPU baseline and parity leg (after the timed region).  Slabs: the start state of the timed

@@ -38,6 +38,7 @@ struct pmc_ctx {
     int* ovf_aux = nullptr;                // second queue: launches on a caller stream (pmc_phase_range_on)
     int* ovf_b = nullptr;                  // third queue: the slab driver's boundary chain
     int* ovf_aux2 = nullptr;               // fourth queue: the slab driver's third interior chain
+    unsigned* run_ctl = nullptr;           // k_subsweep_run's claim heads and row counters (PMC_SLAB_RUNK)
     size_t ovf_bytes = 0;
     int32_t* tmp_cnt = nullptr;
     int32_t* tmp_idx = nullptr;
@@ -283,6 +284,7 @@ void pmc_destroy(pmc_ctx* c) {
     if (c->ovf_aux) (void)hipFree(c->ovf_aux);
     if (c->ovf_b) (void)hipFree(c->ovf_b);
     if (c->ovf_aux2) (void)hipFree(c->ovf_aux2);
+    if (c->run_ctl) (void)hipFree(c->run_ctl);
     if (c->tmp_cnt) (void)hipFree(c->tmp_cnt);
     if (c->tmp_idx) (void)hipFree(c->tmp_idx);
     if (c->d_r) (void)hipFree(c->d_r);
@@ -997,6 +999,10 @@ struct pmc_slab {
         return v;
     }
     std::vector<XferMsg> sends, recvs;    // the exchange being assembled
+    // a z-shift's halo plane not yet exchanged (deferred, PMC_SLAB_DEFER_Z): 0 none, else the shift direction;
+    // the exchange of sweep `pending_sweep`'s first run carries it (same messages plus the counts)
+    int pending_zdir = 0;
+    uint32_t pending_sweep = 0;
     bool messages() const { return comm != nullptr || group != nullptr; }
 };
 
@@ -1028,6 +1034,16 @@ void drop_slab(pmc_ctx* c) {
 // interior [1, nz-1); every inner border is even (a parity-q run of a chain then ends at the same
 // side of each border).  Two chains split at 2*(nz/4), three at the even planes nearest 1/3 and
 // 2/3 of the interior; degenerate splits of thin slabs fold into fewer chains.  Returns the count.
+// PMC_SLAB_RUNK=1: each run's interior planes as ONE dataflow launch (k_subsweep_run) instead of
+// per-phase launches in interior chains
+bool slab_runk() {
+    static const bool on = [] {
+        const char* v = std::getenv("PMC_SLAB_RUNK");
+        return v && std::atoi(v) == 1;
+    }();
+    return on;
+}
+
 int slab_split(int chains, int nz, int zs[4]) {
     zs[0] = 1;
     zs[1] = zs[2] = zs[3] = nz - 1;
@@ -1172,18 +1188,22 @@ int inject_delay(pmc_slab* s) {
 // bottom for p = 1) comes from the other side: one message each way, straight from and into the
 // state buffer (no packing).  The next run (parity 1-p) is the first to read H_p.  A single rank
 // without messages copies its own plane into its periodic halo.  On aux.
-int slab_exchange_run(pmc_ctx* c, int p) {
+int slab_exchange_run(pmc_ctx* c, int p, bool with_counts = false) {
     pmc_slab* s = c->slab;
     const int nz = c->P.nz_local;
-    const size_t pf = plane_floats(c);
+    const size_t pf = plane_floats(c), pc = plane_cells(c);
     const int src = p == 0 ? 0 : nz - 1, dst = p == 0 ? nz : -1;
     if (!s->messages()) {
         PMC_HIP(hipMemcpyAsync(disk_plane(c, dst), disk_plane(c, src), pf * 4, hipMemcpyDeviceToDevice, s->aux));
+        if (with_counts)
+            PMC_HIP(hipMemcpyAsync(n_plane(c, dst), n_plane(c, src), pc * 2, hipMemcpyDeviceToDevice, s->aux));
         return inject_delay(s);
     }
     const int to = p == 0 ? s->below : s->above, from = p == 0 ? s->above : s->below;
     xfer_send(s, disk_plane(c, src), pf * 4, to);
+    if (with_counts) xfer_send(s, n_plane(c, src), pc * 2, to);
     xfer_recv(s, disk_plane(c, dst), pf * 4, from);
+    if (with_counts) xfer_recv(s, n_plane(c, dst), pc * 2, from);
     if (int rc = xfer_run(s)) return rc;
     return inject_delay(s);
 }
@@ -1232,6 +1252,16 @@ int slab_exchange_zplane(pmc_ctx* c, int dir) {
     xfer_recv(s, n_plane(c, dst), pc * 2, from);
     if (int rc = xfer_run(s)) return rc;
     return inject_delay(s);
+}
+
+// A deferred z-shift halo exchange (PMC_SLAB_DEFER_Z) issued now, on T (collective: every rank
+// defers and flushes at the same calls).
+int slab_flush_z(pmc_ctx* c) {
+    pmc_slab* s = c->slab;
+    if (!s || !s->pending_zdir) return PMC_OK;
+    const int dir = s->pending_zdir;
+    s->pending_zdir = 0;
+    return slab_exchange_zplane(c, dir);
 }
 
 }  // namespace
@@ -1396,6 +1426,7 @@ int pmc_slab_init_local(pmc_ctx* c, int rank, pmc_local_group* g) {
 int pmc_slab_exchange(pmc_ctx* c) {
     if (!c || !c->slab) return fail(PMC_ERR_ARG, "no slab driver (pmc_slab_init)");
     pmc_slab* s = c->slab;
+    s->pending_zdir = 0;   // both halos with their counts below: a deferred z exchange is subsumed
     // everything before (state set up on the context stream, earlier sweeps on all three streams)
     // is ordered before the exchange and before every stream's next work
     int rc = slab_join(c);
@@ -1423,11 +1454,24 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
     // (chain 0 on the context stream S); every inner border zs[j] is even, so every parity-q run
     // of a chain ends at the same side of each border
     int zs[4];
-    const int nc = slab_split(s->chains, nz, zs);
+    const bool runk = slab_runk();
+    const int nc = slab_split(runk ? 1 : s->chains, nz, zs);
+    if (runk && !c->run_ctl) {
+        const size_t nb = sizeof(unsigned) * subsweep_run_ctl_ints(c->G);
+        PMC_HIP(hipMalloc(&c->run_ctl, nb));
+        PMC_HIP(hipMemsetAsync(c->run_ctl, 0, nb, S));
+    }
     hipStream_t ist[3] = {S, s->hi[0], s->hi[1]};
     int* iovf[3] = {c->ovf, c->ovf_aux, c->ovf_aux2};
     const pmc_sweep_plan_t plan = pmc_plan_for_sweep_ex(c->P.seed, sweep, c->P.w, c->P.flags);
     int rc;
+    // a deferred z-shift halo exchange: carried by this sweep's first run exchange when this is the
+    // sweep it was deferred to (the first run's boundary plane does not read that halo), else now
+    bool merge_z = false;
+    if (s->pending_zdir) {
+        if (sweep == s->pending_sweep) merge_z = true;
+        else if ((rc = slab_flush_z(c))) return rc;
+    }
     // The 8 colour phases form runs of equal z parity q (two runs of 4 with the default plan).  In a
     // run only the planes of parity q change, each reading its own plane and the parity 1-q planes
     // next to it, which no phase of the run writes and no halo of the run changes: every plane's
@@ -1492,17 +1536,58 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
         // chain, and the other streams wait for it (a stream wait costs a barrier packet on the
         // critical path)
         const bool first = k == 0;
+        // B, then the exchange -- issued first: the boundary chain (its phases, the exchange, the
+        // next run's phases) is the sweep's critical path, so its work reaches the GPU first.  (The
+        // issue order inside a run does not change the dependencies: every wait refers to events of
+        // the previous run.)
+        // (PMC_SLAB_B_FIRST=0: the interior chains first, round 3's order, for A/B)
+        static const bool b_first = [] {
+            const char* v = std::getenv("PMC_SLAB_B_FIRST");
+            return !(v && std::atoi(v) == 0);
+        }();
+        auto boundary = [&]() -> int {
+            const int zb = q == 0 ? 0 : nz - 1;
+            int r;
+            if (!first && (r = border_waits(kB, zb, zb + 1, q, T, p))) return r;
+            if ((r = phases(T, c->ovf_b, zb, zb + 1, k, k1, true))) return r;
+            PMC_HIP(hipEventRecord(s->ev_run[kB][q], T));
+            if ((r = slab_exchange_run(c, q, merge_z))) return r;
+            merge_z = false;
+            s->pending_zdir = 0;
+            return PMC_OK;
+        };
+        if (b_first && (rc = boundary())) return rc;
         for (int j = 0; j < nc; ++j) {
             if (!first && (rc = border_waits(j, zs[j], zs[j + 1], q, ist[j], p))) return rc;
-            if (zs[j + 1] > zs[j] && (rc = phases(ist[j], iovf[j], zs[j], zs[j + 1], k, k1, false))) return rc;
+            if (runk && j == 0) {
+                // the run's interior planes of parity q as one dataflow launch: colour planes cz with
+                // z = 2 cz + q in [1, nz-1)
+                RunDesc rd;
+                rd.nph = k1 - k;
+                rd.oz = q;
+                rd.cz0 = q == 0 ? 1 : 0;                               // (z = 0 is the boundary plane)
+                rd.ncz = nz - 2 - q >= 0 ? (nz - 2 - q) / 2 + 1 - rd.cz0 : 0;  // last z <= nz - 2
+                rd.oxy = 0;
+                for (int kk = k; kk < k1; ++kk) {
+                    int o[3];
+                    pmc_colour_offset(plan.order[kk], o);
+                    rd.oxy |= (o[0] | (o[1] << 1)) << (2 * (kk - k));
+                }
+                if (rd.ncz > 0) {
+                    hipError_t le = launch_run_check(c->G, c->run_ctl, c->ovf, c->flags, true, S);
+                    if (le == hipSuccess) {
+                        LaunchTiming lt;
+                        le = launch_subsweep_run(c->G, c->disk[c->cur], c->n[c->cur], rd, sweep, c->stats, c->ovf,
+                                                 c->run_ctl, c->flags, S, next_timing(c, 0, &lt));
+                    }
+                    if (le != hipSuccess) return hip_fail(le, "run launch");
+                }
+            } else if (zs[j + 1] > zs[j] && (rc = phases(ist[j], iovf[j], zs[j], zs[j + 1], k, k1, false))) {
+                return rc;
+            }
             PMC_HIP(hipEventRecord(s->ev_run[j][q], ist[j]));
         }
-        // B, then the exchange
-        const int zb = q == 0 ? 0 : nz - 1;
-        if (!first && (rc = border_waits(kB, zb, zb + 1, q, T, p))) return rc;
-        if ((rc = phases(T, c->ovf_b, zb, zb + 1, k, k1, true))) return rc;
-        PMC_HIP(hipEventRecord(s->ev_run[kB][q], T));
-        if ((rc = slab_exchange_run(c, q))) return rc;
+        if (!b_first && (rc = boundary())) return rc;
         k = k1;
     }
     // after the 8 phases both halo planes are exact copies of the neighbours' planes, so
@@ -1512,16 +1597,16 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
     // plane next to it), and the other one is received: one plane with its counts, one direction.
     int zl0, zl1;
     const int dir = slab_shift_planes(nz, plan, &zl0, &zl1);
-    // Split shift (PMC_SLAB_SPLIT_SHIFT=1, shifts along x or y): of all the shift's output planes
+    // Split shift (default; PMC_SLAB_SPLIT_SHIFT=0 off; shifts along x or y): of all the shift's output planes
     // only the halo H_q the LAST run's exchange fills reads that exchange (along x/y an output plane
     // reads only itself).  The context stream S shifts every other plane as soon as the interior
     // chains and the boundary chain's last phases are done -- not waiting for the exchange -- and T
     // shifts H_q after it: the exchange leaves the sweep's critical path (it matters once the
     // exchange takes xGMI time: PMC_XFER_DELAY_US rehearsals).  The next sweep's interior chains
     // read no halo; T, which runs the next boundary phases, is in order after its own part.
-    static const bool split_env = [] {
+    static const bool split_env = [] {   // default on (PMC_SLAB_SPLIT_SHIFT=0: off)
         const char* v = std::getenv("PMC_SLAB_SPLIT_SHIFT");
-        return v && std::atoi(v) == 1;
+        return !(v && std::atoi(v) == 0);
     }();
     const int q_last = plan.order[7] % 2;
     const int hq = q_last == 0 ? nz : -1;                    // the halo the last exchange fills
@@ -1558,25 +1643,53 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
     PMC_HIP(hipEventRecord(s->ev_i, S));
     for (int j = 1; j < nc; ++j) PMC_HIP(hipStreamWaitEvent(ist[j], s->ev_i, 0));
     PMC_HIP(hipStreamWaitEvent(T, s->ev_i, 0));
-    if (dir != 0 && (rc = slab_exchange_zplane(c, dir))) return rc;
+    // After a shift along z in direction dir the halo on the +dir side is received: the neighbour's
+    // new plane next to it (plane 0 of the rank above for dir > 0, its top plane nz-1 of the rank
+    // below for dir < 0) -- exactly the plane that neighbour sends as the boundary plane of its
+    // run of parity 0 (dir > 0) or 1 (dir < 0) after that run.  Default (PMC_SLAB_DEFER_Z=0: off): when the next
+    // sweep's first run is that parity, its boundary plane reads only the other halo (the
+    // interior chains read none), so this exchange is skipped and the first run's exchange brings
+    // the plane -- with its counts -- one run later: one exchange (xGMI latency) less on the
+    // exchange stream's chain.  Any other next call flushes it first (slab_flush_z).
+    static const bool defer_env = [] {   // default on (PMC_SLAB_DEFER_Z=0: off)
+        const char* v = std::getenv("PMC_SLAB_DEFER_Z");
+        return !(v && std::atoi(v) == 0);
+    }();
+    if (dir != 0) {
+        const pmc_sweep_plan_t next = pmc_plan_for_sweep_ex(c->P.seed, sweep + 1, c->P.w, c->P.flags);
+        const int q_next = next.order[0] % 2;
+        if (defer_env && q_next == (dir > 0 ? 0 : 1)) {
+            s->pending_zdir = dir;
+            s->pending_sweep = sweep + 1;
+        } else if ((rc = slab_exchange_zplane(c, dir))) {
+            return rc;
+        }
+    }
     PMC_HIP(hipEventRecord(s->ev_x, T));
     return PMC_OK;
 }
 
 int pmc_slab_layout(pmc_ctx* c, int* n_chains, int borders[4]) {
     if (!c || !c->slab || !n_chains || !borders) return fail(PMC_ERR_ARG, "no slab driver (pmc_slab_init)");
-    *n_chains = slab_split(c->slab->chains, c->P.nz_local, borders);
+    *n_chains = slab_split(slab_runk() ? 1 : c->slab->chains, c->P.nz_local, borders);
     return PMC_OK;
 }
 
 int pmc_slab_finish(pmc_ctx* c) {
     if (!c || !c->slab) return fail(PMC_ERR_ARG, "no slab driver (pmc_slab_init)");
-    return slab_join(c);
+    if (int rc = slab_flush_z(c)) return rc;
+    if (int rc = slab_join(c)) return rc;
+    if (c->run_ctl) {   // the last run's checks (every item claimed, no overflowing cell)
+        hipError_t e = launch_run_check(c->G, c->run_ctl, c->ovf, c->flags, true, c->stream);
+        if (e != hipSuccess) return hip_fail(e, "run check");
+    }
+    return PMC_OK;
 }
 
 int pmc_slab_observables(pmc_ctx* c, int with_energy, pmc_stats* out, double* e_out) {
     if (!c || !c->slab || !out || (with_energy && !e_out)) return fail(PMC_ERR_ARG, "bad argument");
     pmc_slab* s = c->slab;
+    if (int rc = slab_flush_z(c)) return rc;   // the energy reads both halos
     pmc_stats st;
     if (int rc = pmc_stats_read(c, &st, 0)) return rc;
     int64_t ef = 0;

@@ -185,20 +185,36 @@ def test_local_group_missing_rank_fails_not_hangs(pmc):
     group.close()
 
 
-@pytest.mark.parametrize("chains,split,world,cps,nz,atoms", [
-    (1, 0, 4, 16, 4, 10_000),
-    (3, 0, 2, 32, 16, 120_000),     # interior chains [1,6), [6,10), [10,15)
-    (3, 0, 4, 32, 8, 120_000),      # [1,4), [4,6), [6,7)
-    (2, 1, 4, 32, 8, 120_000),      # split shift: the last exchange's halo shifted on T
-    (3, 1, 2, 32, 16, 120_000),
+# defaults: split shift and deferred z exchanges on (in the window, sweeps 16 and 17 defer; the last
+# deferred one is flushed by finish)
+_ROUND3 = {"PMC_SLAB_SPLIT_SHIFT": "0", "PMC_SLAB_DEFER_Z": "0"}   # round 3's schedule
+_BFULL = {"PMC_BOUNDARY_FULL": "1"}
+_RUNK = {"PMC_SLAB_RUNK": "1"}      # each run's interior planes as one dataflow launch
+
+
+@pytest.mark.parametrize("chains,env,world,cps,nz,atoms", [
+    (1, {}, 4, 16, 4, 10_000),
+    (3, {}, 2, 32, 16, 120_000),       # interior chains [1,6), [6,10), [10,15)
+    (3, {}, 4, 32, 8, 120_000),        # [1,4), [4,6), [6,7)
+    (2, _ROUND3, 4, 32, 8, 120_000),   # no split shift, no deferral
+    (3, _ROUND3, 2, 32, 16, 120_000),
+    (2, _BFULL, 4, 32, 8, 120_000),    # full-capacity boundary launches
+    (2, _BFULL, 2, 16, 8, 10_000),
+    (1, _RUNK, 4, 32, 8, 120_000),     # 3 interior planes per run: XCDs 0-2 (one plane each)
+    (1, _RUNK, 2, 32, 16, 120_000),    # 7 per run
+    (1, _RUNK, 1, 32, 32, 120_000),    # one rank, 15 per run: two planes on XCDs 0-6
+    (1, _RUNK, 2, 48, 24, 400_000),    # 48^2 planes (24 colour cells per row: 12 waves), 11 per run
 ])
-def test_c_slab_driver_chain_count(pmc, oracle, chains, split, world, cps, nz, atoms):
+def test_c_slab_driver_chain_count(pmc, oracle, chains, env, world, cps, nz, atoms):
     """PMC_SLAB_CHAINS=1 (one interior chain per rank: every phase one launch on the context
-    stream) and =3 (three interior chains on three streams beside the exchange stream), and
-    PMC_SLAB_SPLIT_SHIFT=1 (x/y shifts: the halo the last exchange fills shifted on the exchange
-    stream, every other plane on the context stream without waiting for that exchange), through the
-    in-process transport, equal the oracle's whole box over 8 sweeps with shifts along x, y and z
-    both ways.  Subprocess: the switches are read once per process."""
+    stream) and =3 (three interior chains on three streams beside the exchange stream), with the
+    default split shift (x/y shifts: the halo the last exchange fills shifted on the exchange
+    stream, every other plane on the context stream without waiting for that exchange) and deferred
+    z exchanges (a z shift's halo plane carried by the next sweep's first run exchange when that run
+    does not read it), without both (PMC_SLAB_SPLIT_SHIFT=0, PMC_SLAB_DEFER_Z=0), and with
+    PMC_BOUNDARY_FULL=1 (boundary phases as one full-capacity launch),
+    through the in-process transport, equal the oracle's whole box over 8 sweeps with shifts along
+    x, y and z both ways.  Subprocess: the switches are read once per process."""
     import subprocess
     import sys
     code = r'''
@@ -218,6 +234,7 @@ def main(r):
     keep.append(d)
     lay = d.ctx.slab_layout()
     d.run(first, 8)
+    assert d.ctx.error_flags() == 0, d.ctx.error_flags()
     return d.owned(), d.ctx.stats(), lay
 res = _run_ranks(world, main)
 st = pmc_oracle.OracleState(pmc_oracle.make_params(cps=cps, cps_z=world * nz))
@@ -239,7 +256,7 @@ print("ok")
     out = subprocess.run([sys.executable, "-c", code, os.path.join(repo, "parallel-monte-carlo_amd"),
                           os.path.join(repo, "oracle"), os.path.join(repo, "tests"),
                           str(world), str(cps), str(nz), str(atoms), str(chains)],
-                         env=dict(os.environ, PMC_SLAB_CHAINS=str(chains), PMC_SLAB_SPLIT_SHIFT=str(split)),
+                         env=dict(os.environ, PMC_SLAB_CHAINS=str(chains), **env),
                          capture_output=True, text=True,
                          timeout=300)
     assert out.returncode == 0, out.stderr[-3000:]
