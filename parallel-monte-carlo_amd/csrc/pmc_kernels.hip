@@ -1155,9 +1155,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     uint32_t* __restrict__ flags) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int lane = threadIdx.x & (kWave - 1);
-    const uint32_t x = xcc_id();
     const uint32_t hx = (uint32_t)g.cps_x >> 1, rows = (uint32_t)g.cps_y >> 1;
     const uint32_t wpr = (hx + 1u) >> 1;                      // two-cell waves per colour row
+    const uint32_t x = xcc_id();
     if (x >= 8u) {
         if (lane == 0) atomicOr(flags, 128u);                 // not an 8-XCD (SPX) dispatch
         return;
