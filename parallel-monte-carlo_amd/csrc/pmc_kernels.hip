@@ -646,6 +646,9 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
     constexpr int NB = decltype(nb_c)::value;
     unsigned long long pend = 0;                       // in-cell moves of the current round
     int sp_l = 0;                                      // lane j: row slot of the round's move j
+#ifdef PMC_PROBE_NO_REPEAT_OLD
+    unsigned long long seen = 0;                       // particles evaluated so far in the visit
+#endif
     for (int m0 = 0; m0 < g.n_moves; m0 += (m0 == 0 ? first_len : 16)) {
         if (m0 > 0) rng_single(m0);
         const int clen = m0 == 0 ? first_len : 16;
@@ -711,11 +714,26 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
                     if (__builtin_amdgcn_inverse_ballot_w64(mo)) buf[mbcnt64_add(mo, cn)] = r2on;
                     C = cn + __popcll(mo);
                 };
+#ifdef PMC_PROBE_NO_REPEAT_OLD
+                // timing probe only (wrong results): a particle's 2nd and later evaluated move of
+                // the visit lists no old-position terms -- the most a cached old energy could save
+                const bool rep = (seen & sbit) != 0ull;
+                seen |= sbit;
+#endif
                 auto block = [&](int base, unsigned long long excl) {
                     // slots >= K hold +inf in x: their r2 is inf, never listed; the moving slot
                     // (block 0) is cleared from the masks by excl
                     const int k = base + lane;
                     const float xj = px_[k], yj = py_[k], zj = pz_[k];
+#ifdef PMC_PROBE_NO_REPEAT_OLD
+                    if (rep) {
+                        const float r2n = pmc_r2(qx - xj, qy - yj, qz - zj);
+                        const unsigned long long mn = __builtin_amdgcn_ballot_w64(r2n <= rc2) & ~excl;
+                        if (__builtin_amdgcn_inverse_ballot_w64(mn)) buf[mbcnt64_add(mn, C)] = r2n;
+                        C += __popcll(mn);
+                        return;
+                    }
+#endif
                     // old-position term computed negated (= -r2o bit for bit, pmc_r2_neg):
                     // listed with its sign bit set at no extra instruction
                     list(pmc_r2(qx - xj, qy - yj, qz - zj), pmc_r2_neg(xi - xj, yi - yj, zi - zj), excl);
@@ -1418,6 +1436,16 @@ __global__ __launch_bounds__(kWave) void k_sweep_small(DevGeom g, float* __restr
 #endif
 constexpr int kShiftThreads = PMC_SHIFT_THREADS;
 
+// PMC_SHIFT_NT=1: the output rows as nontemporal stores (streamed past the L2, which then keeps
+// the input rows the neighbour reads re-fetch)
+__device__ __forceinline__ void shift_store(float* p, float v) {
+#if PMC_SHIFT_NT
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+
 template <int NSLOT, int U>
 __global__ __launch_bounds__(kShiftThreads) void k_shift(DevGeom g, const float* __restrict__ din,
                                                const int16_t* __restrict__ nin, float* __restrict__ dout,
@@ -1543,7 +1571,7 @@ __global__ __launch_bounds__(kShiftThreads) void k_shift(DevGeom g, const float*
             if (dst < nm) {
 #pragma unroll
                 for (int dim = 0; dim < 3; ++dim)
-                    dout[ob + (uint64_t)(dim * nm + dst)] = (dim == f) ? D + offset[j] : own[j][dim];
+                    shift_store(dout + ob + (uint64_t)(dim * nm + dst), (dim == f) ? D + offset[j] : own[j][dim]);
             }
         }
         if (take) {
@@ -1551,7 +1579,7 @@ __global__ __launch_bounds__(kShiftThreads) void k_shift(DevGeom g, const float*
             if (dst < nm) {
 #pragma unroll
                 for (int dim = 0; dim < 3; ++dim)
-                    dout[ob + (uint64_t)(dim * nm + dst)] = (dim == f) ? ((Dn + offset[j]) + s) : nbv[j][dim];   // own offset (VS shiftCells.h:96)
+                    shift_store(dout + ob + (uint64_t)(dim * nm + dst), (dim == f) ? ((Dn + offset[j]) + s) : nbv[j][dim]);   // own offset (VS shiftCells.h:96)
             }
         }
         if (live[j] && p == 0) {
