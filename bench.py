@@ -64,12 +64,13 @@ def stencil_counts(n: np.ndarray, cps: tuple[int, int, int]) -> np.ndarray:
     return s.reshape(-1)
 
 
-def slab_stencil_counts(n_storage: np.ndarray, cps: int, nz: int) -> np.ndarray:
-    """S_c of the owned cells of a slab (storage planes 0 and nz+1 are the halos)."""
-    g = n_storage.astype(np.int64).reshape(nz + 2, cps, cps)
+def slab_stencil_counts(n_storage: np.ndarray, cps: int, nz: int, halo: int = 1) -> np.ndarray:
+    """S_c of the owned cells of a slab (storage planes [0, halo) and [nz+halo, nz+2*halo) are the
+    halos)."""
+    g = n_storage.astype(np.int64).reshape(nz + 2 * halo, cps, cps)
     s = np.zeros((nz, cps, cps), np.int64)
     for dz in (-1, 0, 1):
-        sub = g[1 + dz:1 + dz + nz]
+        sub = g[halo + dz:halo + dz + nz]
         for dy in (-1, 0, 1):
             for dx in (-1, 0, 1):
                 s += np.roll(sub, shift=(-dy, -dx), axis=(1, 2))
@@ -253,13 +254,13 @@ def parity_leg_slab(ctx, one_sweep, finish, disk_s, n_s, sweep0: int, e0: float,
             "gpu_side": "all ranks (slab driver), owned planes gathered on rank 0"}
 
 
-def make_gather(world: int, rank: int, plane: int, nz: int, row: int):
+def make_gather(world: int, rank: int, plane: int, nz: int, row: int, halo: int = 1):
     """gather(disk_storage, n_storage) -> (disk, n) of the whole box on rank 0 (None elsewhere): the
     owned planes of every rank in rank order (rank r owns global planes [r*nz, (r+1)*nz)).
     Collective; counts travel as bytes (RCCL has no 16-bit integer type)."""
     def gather(disk_s, n_s):
-        own_d = np.ascontiguousarray(disk_s[plane * row:(nz + 1) * plane * row])
-        own_n = np.ascontiguousarray(n_s[plane:(nz + 1) * plane])
+        own_d = np.ascontiguousarray(disk_s[halo * plane * row:(nz + halo) * plane * row])
+        own_n = np.ascontiguousarray(n_s[halo * plane:(nz + halo) * plane])
         if world == 1:
             return own_d, own_n
         import torch
@@ -379,6 +380,9 @@ def main() -> int:
     ap.add_argument("--xfer-delay-us", type=float, default=0.0,
                     help="slab rehearsals: hold the exchange stream busy this long after every halo exchange "
                          "(PMC_XFER_DELAY_US: the xGMI time and RCCL latency a one-GPU run does not pay)")
+    ap.add_argument("--halo", type=int, default=0, choices=(0, 1, 2),
+                    help="slab halo planes per side: 2 = one exchange per sweep, the neighbour's boundary plane "
+                         "visited redundantly (0: PMC_SLAB_HALO, default 1)")
     args = ap.parse_args()
     if args.xfer_delay_us > 0:
         os.environ["PMC_XFER_DELAY_US"] = str(args.xfer_delay_us)   # read by libpmc at its first exchange
@@ -458,7 +462,8 @@ def main() -> int:
         # the product multi-GPU path: sweep schedule + RCCL halo exchange in C (pmc_slab_*)
         from pmc_amd.slab import SlabDriver
         use_rccl = world > 1 or args.self_rccl or (config == "5" and not args.local_halo)
-        drv = SlabDriver(cps=cps, nz_local=nz_local, rank=rank, world=world, stream=stream, use_rccl=use_rccl)
+        drv = SlabDriver(cps=cps, nz_local=nz_local, rank=rank, world=world, stream=stream, use_rccl=use_rccl,
+                         halo=args.halo)
         if config == "5" or args.emulate_ranks:
             drv.ctx.init_lattice_planes(atoms, cps)     # this rank's planes of the 256^3 / 8e7 (128^3 / 1e7) lattice
         else:
@@ -470,7 +475,9 @@ def main() -> int:
             drv.sweep(s)
 
         finish = drv.finish
-        transport = (f"z-slab x{world}, {nz_local} planes per rank, halo planes over "
+        transport = (f"z-slab x{world}, {nz_local} planes per rank, "
+                     + ("two halo planes per side (one exchange per sweep), " if drv.halo == 2 else "")
+                     + "halo planes over "
                      + ("RCCL (C slab driver)" if use_rccl else "local copies (C slab driver)"))
 
     # warmup
@@ -502,8 +509,8 @@ def main() -> int:
         sub_launch_bytes = staged_bytes(n_owned, stencil) / 8.0
         roof_kernel = "k_subsweep<16,16,true> (one colour phase of the whole box)"
     else:
-        n_owned = n_h[plane:plane * (nz_local + 1)].astype(np.int64)
-        stencil = slab_stencil_counts(n_h, cps, nz_local)
+        n_owned = n_h[plane * drv.halo:plane * (nz_local + drv.halo)].astype(np.int64)
+        stencil = slab_stencil_counts(n_h, cps, nz_local, drv.halo)
         # kind-0 launches: the interior chains (pmc_slab_layout: 1-3 chains, PMC_SLAB_CHAINS), one
         # launch per chain and colour phase; the roofline's bytes per launch are their mean (the
         # chains run concurrently)
@@ -637,7 +644,7 @@ def main() -> int:
                 except Exception as e:  # the baseline is reported, never the measured value
                     cpu = {"error": repr(e)}
         else:
-            gather = make_gather(world, rank, plane, nz_local, 3 * 16)
+            gather = make_gather(world, rank, plane, nz_local, 3 * 16, drv.halo)
             whole = gather(disk_h, n_h)
             if rank == 0:
                 try:

@@ -87,7 +87,9 @@ int normalise(pmc_params* p) {
         return fail(PMC_ERR_ARG, "cells per side, nz_local and z0 must be even (checkerboard)");
     if (p->nmax < 1 || p->nmax > 64) return fail(PMC_ERR_ARG, "nmax must be in 1..64");
     if (p->n_moves < 0) return fail(PMC_ERR_ARG, "n_moves must be >= 0");
-    if (p->halo != 0 && p->halo != 1) return fail(PMC_ERR_ARG, "halo must be 0 or 1");
+    if (p->halo < 0 || p->halo > 2) return fail(PMC_ERR_ARG, "halo must be 0, 1 or 2");
+    if (p->halo == 2 && (p->flags & PMC_FLAG_FULL_SHUFFLE))
+        return fail(PMC_ERR_ARG, "two-plane halos need the grouped colour order (two runs per sweep)");
     if (p->flags & ~PMC_FLAG_FULL_SHUFFLE) return fail(PMC_ERR_ARG, "unknown flags");
     if (!p->halo && (p->nz_local != p->cps_z || p->z0 != 0))
         return fail(PMC_ERR_ARG, "halo == 0 requires the whole box (nz_local == cps_z, z0 == 0)");
@@ -495,7 +497,7 @@ int pmc_shift(pmc_ctx* c, uint32_t sweep) {
 
 int pmc_shift_slab(pmc_ctx* c, uint32_t sweep, int* halo_recv) {
     if (!c || !halo_recv) return fail(PMC_ERR_ARG, "null argument");
-    if (!c->P.halo) return fail(PMC_ERR_ARG, "pmc_shift_slab needs a slab context (halo = 1)");
+    if (c->P.halo != 1) return fail(PMC_ERR_ARG, "pmc_shift_slab needs a slab context (halo = 1)");
     const pmc_sweep_plan_t plan = pmc_plan_for_sweep_ex(c->P.seed, sweep, c->P.w, c->P.flags);
     int zl0, zl1;
     *halo_recv = slab_shift_planes(c->P.nz_local, plan, &zl0, &zl1);
@@ -767,7 +769,7 @@ namespace {
 // owned cells of the storage (slab mode skips the halo planes)
 void owned_range(const pmc_ctx* c, int64_t* first, int64_t* count) {
     const int64_t plane = (int64_t)c->P.cps_x * c->P.cps_y;
-    *first = c->P.halo ? plane : 0;
+    *first = plane * c->P.halo;
     *count = plane * c->P.nz_local;
 }
 
@@ -999,6 +1001,14 @@ struct pmc_slab {
         return v;
     }
     std::vector<XferMsg> sends, recvs;    // the exchange being assembled
+    // two-plane halos (pmc_params.halo = 2, slab_sweep_h2): the stream that visits the neighbour's
+    // boundary plane redundantly ("R"), the shifted send planes (planes 0, 1 then nz-2, nz-1, with
+    // their counts) and the counters those redundant visits add to (never read)
+    hipStream_t hr = nullptr;
+    float* send_d = nullptr;
+    int16_t* send_n = nullptr;
+    unsigned long long* stats_scratch = nullptr;
+    hipEvent_t ev_hp = nullptr;           // T after a boundary plane it shifted itself
     // a z-shift's halo plane not yet exchanged (deferred, PMC_SLAB_DEFER_Z): 0 none, else the shift direction;
     // the exchange of sweep `pending_sweep`'s first run carries it (same messages plus the counts)
     int pending_zdir = 0;
@@ -1020,7 +1030,13 @@ void drop_slab(pmc_ctx* c) {
     if (s->aux) (void)hipStreamDestroy(s->aux);
     for (hipStream_t h : s->hi)
         if (h) (void)hipStreamSynchronize(h);
-    for (hipEvent_t e : {s->ev_i, s->ev_b, s->ev_t, s->ev_x})
+    if (s->hr) {
+        (void)hipStreamSynchronize(s->hr);
+        (void)hipStreamDestroy(s->hr);
+    }
+    for (void* m : {(void*)s->send_d, (void*)s->send_n, (void*)s->stats_scratch})
+        if (m) (void)hipFree(m);
+    for (hipEvent_t e : {s->ev_i, s->ev_b, s->ev_t, s->ev_x, s->ev_hp})
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t* e : s->run_events())
         if (*e) (void)hipEventDestroy(*e);
@@ -1065,7 +1081,7 @@ int slab_split(int chains, int nz, int zs[4]) {
 int slab_join(pmc_ctx* c) {
     pmc_slab* s = c->slab;
     if (!s) return PMC_OK;
-    for (hipStream_t st : {s->aux, s->hi[0], s->hi[1]}) {
+    for (hipStream_t st : {s->aux, s->hi[0], s->hi[1], s->hr}) {
         if (!st) continue;
         hipError_t e = hipEventRecord(s->ev_b, st);
         if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, s->ev_b, 0);
@@ -1156,9 +1172,9 @@ int xfer_run(pmc_slab* s) {
 
 size_t plane_floats(const pmc_ctx* c) { return (size_t)c->P.cps_x * c->P.cps_y * 3 * c->P.nmax; }
 size_t plane_cells(const pmc_ctx* c) { return (size_t)c->P.cps_x * c->P.cps_y; }
-// storage plane of local plane z (-1 = bottom halo, nz_local = top halo)
-float* disk_plane(pmc_ctx* c, int z) { return c->disk[c->cur] + (size_t)(z + 1) * plane_floats(c); }
-int16_t* n_plane(pmc_ctx* c, int z) { return c->n[c->cur] + (size_t)(z + 1) * plane_cells(c); }
+// storage plane of local plane z (-halo .. -1 bottom halos, nz_local .. nz_local-1+halo top halos)
+float* disk_plane(pmc_ctx* c, int z) { return c->disk[c->cur] + (size_t)(z + c->P.halo) * plane_floats(c); }
+int16_t* n_plane(pmc_ctx* c, int z) { return c->n[c->cur] + (size_t)(z + c->P.halo) * plane_cells(c); }
 
 
 // Strong-scaling rehearsal (PMC_XFER_DELAY_US, microseconds, default 0): after every halo exchange
@@ -1208,28 +1224,37 @@ int slab_exchange_run(pmc_ctx* c, int p, bool with_counts = false) {
     return inject_delay(s);
 }
 
-// both boundary planes with their counts (after shiftCells / initialisation), on aux
-int slab_exchange_full(pmc_ctx* c) {
+// both halos with their counts, halo (1 or 2) planes deep: the owned planes [0, h) go down and
+// [nz-h, nz) up, the halos [nz, nz+h) come from above and [-h, 0) from below.  Sources: the state
+// buffer (initialisation, restart) or, with from_send, the send buffer T shifted them into
+// (two-plane halos after shiftCells: the interior chains may already be rewriting planes 1 and
+// nz-2 of the state).  On aux.
+int slab_exchange_full(pmc_ctx* c, bool from_send = false) {
     pmc_slab* s = c->slab;
-    const int nz = c->P.nz_local;
+    const int nz = c->P.nz_local, h = c->P.halo;
     const size_t pf = plane_floats(c), pc = plane_cells(c);
+    const float* lo_d = from_send ? s->send_d : disk_plane(c, 0);
+    const float* hi_d = from_send ? s->send_d + (size_t)h * pf : disk_plane(c, nz - h);
+    const int16_t* lo_n = from_send ? s->send_n : n_plane(c, 0);
+    const int16_t* hi_n = from_send ? s->send_n + (size_t)h * pc : n_plane(c, nz - h);
+    const size_t db = (size_t)h * pf * 4, nb = (size_t)h * pc * 2;
     if (!s->messages()) {
-        PMC_HIP(hipMemcpyAsync(disk_plane(c, nz), disk_plane(c, 0), pf * 4, hipMemcpyDeviceToDevice, s->aux));
-        PMC_HIP(hipMemcpyAsync(n_plane(c, nz), n_plane(c, 0), pc * 2, hipMemcpyDeviceToDevice, s->aux));
-        PMC_HIP(hipMemcpyAsync(disk_plane(c, -1), disk_plane(c, nz - 1), pf * 4, hipMemcpyDeviceToDevice, s->aux));
-        PMC_HIP(hipMemcpyAsync(n_plane(c, -1), n_plane(c, nz - 1), pc * 2, hipMemcpyDeviceToDevice, s->aux));
+        PMC_HIP(hipMemcpyAsync(disk_plane(c, nz), lo_d, db, hipMemcpyDeviceToDevice, s->aux));
+        PMC_HIP(hipMemcpyAsync(n_plane(c, nz), lo_n, nb, hipMemcpyDeviceToDevice, s->aux));
+        PMC_HIP(hipMemcpyAsync(disk_plane(c, -h), hi_d, db, hipMemcpyDeviceToDevice, s->aux));
+        PMC_HIP(hipMemcpyAsync(n_plane(c, -h), hi_n, nb, hipMemcpyDeviceToDevice, s->aux));
         return PMC_OK;
     }
-    // per peer, sends and receives match in issue order: (plane, counts) down, then up
+    // per peer, sends and receives match in issue order: (planes, counts) down, then up
     // (counts travel as bytes: RCCL has no 16-bit integer type)
-    xfer_send(s, disk_plane(c, 0), pf * 4, s->below);
-    xfer_send(s, n_plane(c, 0), pc * 2, s->below);
-    xfer_send(s, disk_plane(c, nz - 1), pf * 4, s->above);
-    xfer_send(s, n_plane(c, nz - 1), pc * 2, s->above);
-    xfer_recv(s, disk_plane(c, nz), pf * 4, s->above);
-    xfer_recv(s, n_plane(c, nz), pc * 2, s->above);
-    xfer_recv(s, disk_plane(c, -1), pf * 4, s->below);
-    xfer_recv(s, n_plane(c, -1), pc * 2, s->below);
+    xfer_send(s, lo_d, db, s->below);
+    xfer_send(s, lo_n, nb, s->below);
+    xfer_send(s, hi_d, db, s->above);
+    xfer_send(s, hi_n, nb, s->above);
+    xfer_recv(s, disk_plane(c, nz), db, s->above);
+    xfer_recv(s, n_plane(c, nz), nb, s->above);
+    xfer_recv(s, disk_plane(c, -h), db, s->below);
+    xfer_recv(s, n_plane(c, -h), nb, s->below);
     return xfer_run(s);
 }
 
@@ -1286,7 +1311,7 @@ namespace {
 // common part of pmc_slab_init / pmc_slab_init_local: streams, events, overflow queue, buffers
 int slab_attach(pmc_ctx* c, int rank, int world, bool messages) {
     if (!c || world < 1 || rank < 0 || rank >= world) return fail(PMC_ERR_ARG, "bad argument");
-    if (c->P.halo != 1) return fail(PMC_ERR_ARG, "pmc_slab_init needs a slab context (halo = 1)");
+    if (c->P.halo < 1) return fail(PMC_ERR_ARG, "pmc_slab_init needs a slab context (halo = 1 or 2)");
     if (c->P.nz_local < 2 || c->P.z0 != rank * c->P.nz_local || c->P.cps_z != world * c->P.nz_local)
         return fail(PMC_ERR_ARG, "slab geometry must be z0 = rank*nz_local, cps_z = world*nz_local");
     PMC_HIP(hipStreamSynchronize(c->stream));
@@ -1311,7 +1336,7 @@ int slab_attach(pmc_ctx* c, int rank, int world, bool messages) {
         drop_slab(c);
         return hip_fail(e, "hipStreamCreate");
     }
-    std::vector<hipEvent_t*> evs = {&s->ev_i, &s->ev_b, &s->ev_t, &s->ev_x};
+    std::vector<hipEvent_t*> evs = {&s->ev_i, &s->ev_b, &s->ev_t, &s->ev_x, &s->ev_hp};
     for (hipEvent_t* ev : s->run_events()) evs.push_back(ev);
     for (hipEvent_t* ev : evs)
         if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) {
@@ -1327,6 +1352,22 @@ int slab_attach(pmc_ctx* c, int rank, int world, bool messages) {
             return v ? std::atoi(v) : 0;
         }();
         s->chains = forced >= 1 && forced <= 3 ? forced : 2;
+    }
+    // two-plane halos: at most 2 interior chains -- the redundant halo plane takes the fourth stream
+    if (c->P.halo == 2) {
+        if (s->chains > 2) s->chains = 2;
+        if ((e = hipStreamCreateWithPriority(&s->hr, hipStreamNonBlocking, prio ? hi_p : 0)) != hipSuccess) {
+            drop_slab(c);
+            return hip_fail(e, "hipStreamCreate");
+        }
+        const size_t sb = sizeof(unsigned long long) * kStatCounters * kStatSlots;
+        if ((e = hipMalloc(&s->send_d, 4 * plane_floats(c) * sizeof(float))) != hipSuccess ||
+            (e = hipMalloc(&s->send_n, 4 * plane_cells(c) * sizeof(int16_t))) != hipSuccess ||
+            (e = hipMalloc(&s->stats_scratch, sb)) != hipSuccess ||
+            (e = hipMemsetAsync(s->stats_scratch, 0, sb, c->stream)) != hipSuccess) {
+            drop_slab(c);
+            return hip_fail(e, "hipMalloc (two-plane halos)");
+        }
     }
     for (int j = 0; j + 1 < s->chains; ++j)
         if ((e = hipStreamCreateWithFlags(&s->hi[j], hipStreamNonBlocking)) != hipSuccess) {
@@ -1433,20 +1474,176 @@ int pmc_slab_exchange(pmc_ctx* c) {
     if (rc) return rc;
     PMC_HIP(hipEventRecord(s->ev_i, c->stream));
     PMC_HIP(hipStreamWaitEvent(s->aux, s->ev_i, 0));
-    for (hipStream_t h : s->hi)
+    for (hipStream_t h : {s->hi[0], s->hi[1], s->hr})
         if (h) PMC_HIP(hipStreamWaitEvent(h, s->ev_i, 0));
     if ((rc = slab_exchange_full(c))) return rc;
     PMC_HIP(hipEventRecord(s->ev_t, s->aux));
     PMC_HIP(hipStreamWaitEvent(c->stream, s->ev_t, 0));
-    for (hipStream_t h : s->hi)
+    for (hipStream_t h : {s->hi[0], s->hi[1], s->hr})
         if (h) PMC_HIP(hipStreamWaitEvent(h, s->ev_t, 0));
     PMC_HIP(hipEventRecord(s->ev_x, s->aux));
     for (hipEvent_t* ev : s->run_events()) PMC_HIP(hipEventRecord(*ev, s->aux));
     return PMC_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// Two-plane halos (pmc_params.halo = 2): ONE exchange per sweep, after shiftCells, instead of one
+// per run.  A rank stores two halo planes on each side.  In a sweep's first run (parity a) the
+// halo plane of parity a -- the neighbour's boundary plane P_a, top halo nz for a = 0, bottom halo
+// -1 for a = 1 -- is visited here as well, redundantly, on its own stream R: its cells read only
+// our boundary plane and the second halo plane beyond it, which no phase of that run changes, and
+// its random numbers, cell centre and staging are the owner's (global cell ids), so the result is
+// the owner's bit for bit (its counters go to a scratch buffer: the owner counts them).  The second
+// run's boundary plane P_b reads exactly that halo, so no exchange is needed between the runs.
+// After the two runs the other halos are stale; shiftCells of the owned planes needs only the
+// halo on its dir side along z, which is the fresh one unless (a = 0 and dir < 0) or (a = 1 and
+// dir > 0): then ONE plane is exchanged first (slab_exchange_run of the second run's parity) and T
+// shifts the plane that reads it.  T also shifts the four planes the neighbours need (0, 1, nz-2,
+// nz-1) into a send buffer -- the interior chains may rewrite planes 1 and nz-2 while the exchange
+// is in flight -- and exchanges all four halo planes with their counts.  The next sweep's interior
+// chains read no halo, so they start right after the shift; only T (its boundary plane) and R (the
+// halo plane) wait for the exchange.  Streams: S + one interior stream, T, R (4 hardware queues).
+int slab_sweep_h2(pmc_ctx* c, uint32_t sweep) {
+    pmc_slab* s = c->slab;
+    hipStream_t S = c->stream, T = s->aux, R = s->hr;
+    const int nz = c->P.nz_local;
+    int zs[4];
+    const int nc = slab_split(s->chains, nz, zs);   // <= 2 chains
+    hipStream_t ist[2] = {S, s->hi[0]};
+    int* iovf[2] = {c->ovf, c->ovf_aux};
+    const pmc_sweep_plan_t plan = pmc_plan_for_sweep_ex(c->P.seed, sweep, c->P.w, c->P.flags);
+    const int a = plan.order[0] % 2, b = 1 - a;
+    for (int k = 1; k < 8; ++k)
+        if (plan.order[k] % 2 != (k < 4 ? a : b))
+            return fail(PMC_ERR_ARG, "two-plane halos need the grouped colour order (two runs per sweep)");
+    constexpr int kB = pmc_slab::kB, kR = 2;             // ev_run rows: chains 0-1, R, T
+    const int pa = a == 0 ? 0 : nz - 1, pb = b == 0 ? 0 : nz - 1;   // boundary planes of the runs
+    const int za = a == 0 ? nz : -1;                     // the halo plane R visits in run a
+    auto phases = [&](hipStream_t st, int* ovf, unsigned long long* stats, int z0, int z1, int k0, int k1,
+                      bool plane) -> int {
+        for (int kk = k0; kk < k1; ++kk) {
+            int o[3];
+            pmc_colour_offset(plan.order[kk], o);
+            LaunchTiming lt;
+            hipError_t le = plane ? launch_subsweep_plane(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep,
+                                                          stats, ovf, z0, st, stats == c->stats ? next_timing(c, 2, &lt) : nullptr)
+                                  : launch_subsweep(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep, stats,
+                                                    ovf, z0, z1, st, next_timing(c, 0, &lt));
+            if (le != hipSuccess) return hip_fail(le, "subsweep launch");
+        }
+        return PMC_OK;
+    };
+    auto owner = [&](int z) {
+        if (z == 0 || z == nz - 1) return kB;
+        if (z == za) return kR;
+        int j = 0;
+        while (j + 1 < nc && z >= zs[j + 1]) ++j;
+        return j;
+    };
+    // run b waits for the run-a owners of the planes next to the ones a chain writes
+    auto waits_b = [&](int chain, int z0, int z1, hipStream_t st) -> int {
+        bool need[4] = {false, false, false, false};
+        for (int z = z0; z < z1; ++z) {
+            if ((z & 1) != b) continue;
+            for (int zn : {z - 1, z + 1})
+                if (zn >= -1 && zn <= nz && owner(zn) != chain && (zn >= 0 && zn < nz ? true : zn == za))
+                    need[owner(zn)] = true;
+        }
+        for (int j = 0; j < 4; ++j)
+            if (need[j]) PMC_HIP(hipStreamWaitEvent(st, s->ev_run[j][a], 0));
+        return PMC_OK;
+    };
+    int rc;
+    // ---- run a: T the boundary plane, R the halo plane of parity a, the interior chains --------
+    if ((rc = phases(T, c->ovf_b, c->stats, pa, pa + 1, 0, 4, true))) return rc;
+    PMC_HIP(hipEventRecord(s->ev_run[kB][a], T));
+    PMC_HIP(hipStreamWaitEvent(R, s->ev_x, 0));         // the last exchange filled the halos R reads
+    if ((rc = phases(R, c->ovf_aux2, s->stats_scratch, za, za + 1, 0, 4, true))) return rc;
+    PMC_HIP(hipEventRecord(s->ev_run[kR][a], R));
+    for (int j = 0; j < nc; ++j) {
+        if (zs[j + 1] > zs[j] && (rc = phases(ist[j], iovf[j], c->stats, zs[j], zs[j + 1], 0, 4, false))) return rc;
+        PMC_HIP(hipEventRecord(s->ev_run[j][a], ist[j]));
+    }
+    // ---- run b: T the other boundary plane (it reads R's halo plane), the interior chains -------
+    if ((rc = waits_b(kB, pb, pb + 1, T))) return rc;
+    if ((rc = phases(T, c->ovf_b, c->stats, pb, pb + 1, 4, 8, true))) return rc;
+    PMC_HIP(hipEventRecord(s->ev_run[kB][b], T));
+    for (int j = 0; j < nc; ++j) {
+        if ((rc = waits_b(j, zs[j], zs[j + 1], ist[j]))) return rc;
+        if (zs[j + 1] > zs[j] && (rc = phases(ist[j], iovf[j], c->stats, zs[j], zs[j + 1], 4, 8, false))) return rc;
+        PMC_HIP(hipEventRecord(s->ev_run[j][b], ist[j]));
+    }
+    // ---- shiftCells --------------------------------------------------------------------------
+    const int dir = plan.d <= 0.0f ? -1 : 1;
+    const bool stale = plan.f == 2 && ((a == 0 && dir < 0) || (a == 1 && dir > 0));
+    const int hp = dir < 0 ? 0 : nz - 1;                 // (stale) the plane that reads the stale halo
+    // T: the stale halo first (the neighbour's second-run boundary plane), then the send planes
+    if (stale && (rc = slab_exchange_run(c, b))) return rc;
+    for (int j = 0; j < nc; ++j) PMC_HIP(hipStreamWaitEvent(T, s->ev_run[j][b], 0));
+    PMC_HIP(hipStreamWaitEvent(T, s->ev_run[kR][a], 0));
+    // S: every owned plane (but hp when T shifts it), after every chain, R and T's second run
+    for (int j = 1; j < nc; ++j) PMC_HIP(hipStreamWaitEvent(S, s->ev_run[j][b], 0));
+    PMC_HIP(hipStreamWaitEvent(S, s->ev_run[kR][a], 0));
+    PMC_HIP(hipStreamWaitEvent(S, s->ev_run[kB][b], 0));
+    float* dn = c->disk[c->cur ^ 1];
+    int16_t* nn = c->n[c->cur ^ 1];
+    const float* din = c->disk[c->cur];
+    const int16_t* nin = c->n[c->cur];
+    LaunchTiming lts;
+    hipError_t e = launch_shift_planes(c->G, din, nin, dn, nn, plan.f, plan.d, c->flags, stale && hp == 0 ? 1 : 0,
+                                       stale && hp == nz - 1 ? nz - 1 : nz, S, next_timing(c, 1, &lts));
+    if (e != hipSuccess) return hip_fail(e, "shift launch");
+    if (stale) {
+        e = launch_shift_planes(c->G, din, nin, dn, nn, plan.f, plan.d, c->flags, hp, hp + 1, T, nullptr);
+        if (e != hipSuccess) return hip_fail(e, "shift launch (boundary)");
+        PMC_HIP(hipEventRecord(s->ev_hp, T));
+    }
+    // the send planes: shiftCells of planes [0, 2) and [nz-2, nz) again, into the send buffer (the
+    // kernel addresses its output by storage plane: the base is offset so plane 0 / nz-2 lands at
+    // the buffer's start / third plane)
+    {
+        const int h = c->P.halo;
+        const ptrdiff_t pf = (ptrdiff_t)plane_floats(c), pc = (ptrdiff_t)plane_cells(c);
+        for (int part = 0; part < 2; ++part) {
+            const int z0 = part == 0 ? 0 : nz - 2;
+            float* bd = reinterpret_cast<float*>(reinterpret_cast<uintptr_t>(s->send_d) +
+                                                 (uintptr_t)((2 * part - z0 - h) * pf * (ptrdiff_t)sizeof(float)));
+            int16_t* bn = reinterpret_cast<int16_t*>(reinterpret_cast<uintptr_t>(s->send_n) +
+                                                     (uintptr_t)((2 * part - z0 - h) * pc * (ptrdiff_t)sizeof(int16_t)));
+            e = launch_shift_planes(c->G, din, nin, bd, bn, plan.f, plan.d, c->flags, z0, z0 + 2, T, nullptr);
+            if (e != hipSuccess) return hip_fail(e, "shift launch (send planes)");
+        }
+    }
+    c->cur ^= 1;
+    // ---- the sweep's exchange: all four halo planes with their counts, from the send buffer ----
+    if ((rc = slab_exchange_full(c, true))) return rc;
+    if ((rc = inject_delay(s))) return rc;
+    PMC_HIP(hipEventRecord(s->ev_x, T));
+    // the next sweep: the interior chains after the shift (they read no halo), T and R after it too
+    // (their planes read the shifted owned planes); R also after the exchange (ev_x, next run a);
+    // the chain next to a boundary plane T shifted also after that
+    PMC_HIP(hipEventRecord(s->ev_i, S));
+    for (int j = 1; j < nc; ++j) PMC_HIP(hipStreamWaitEvent(ist[j], s->ev_i, 0));
+    PMC_HIP(hipStreamWaitEvent(T, s->ev_i, 0));
+    PMC_HIP(hipStreamWaitEvent(R, s->ev_i, 0));
+    if (stale) {
+        const int zn = hp == 0 ? 1 : nz - 2;              // the owned plane next to hp
+        const int j = owner(zn);
+        if (zn >= 0 && zn < nz && j < nc) PMC_HIP(hipStreamWaitEvent(ist[j], s->ev_hp, 0));
+    }
+    return PMC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
 int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
     if (!c || !c->slab) return fail(PMC_ERR_ARG, "no slab driver (pmc_slab_init)");
+    if (c->P.halo == 2) return slab_sweep_h2(c, sweep);
     pmc_slab* s = c->slab;
     hipStream_t S = c->stream, T = s->aux;
     const int nz = c->P.nz_local;

@@ -90,6 +90,12 @@ hipError_t launch_subsweep_boundary(const DevGeom& g, float* disk, const int16_t
                                     uint32_t sweep, unsigned long long* stats, int* ovf, int zl_begin, int zl_end,
                                     float* mirror, int mirror_mode, hipStream_t st,
                                     const LaunchTiming* tm = nullptr);
+// one colour plane zl of the storage, halo planes included (the two-plane-halo slab schedule
+// visits the neighbour's boundary plane redundantly; its cell ids and centres are the owner's):
+// the boundary path, one cell per wave + fallback on `ovf`
+hipError_t launch_subsweep_plane(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
+                                 uint32_t sweep, unsigned long long* stats, int* ovf, int zl, hipStream_t st,
+                                 const LaunchTiming* tm = nullptr);
 int subsweep_capacity(const DevGeom& g);
 // whole sweeps of a small whole box in one launch on XCD 0 (k_sweep_small); bar: one unsigned of
 // scratch; cur: the current buffer of the (disk, n) pairs; returns hipErrorInvalidValue when the box

@@ -328,6 +328,12 @@ __device__ __forceinline__ CellGeo cell_geo(const DevGeom& g, int p, int cz0, in
     cg.y = 2 * cg.tb + oy;
     cg.zl = 2 * tc + oz;
     cg.zg0 = g.z0 + cg.zl;
+    // a halo plane visited redundantly (two-plane halos, launch_subsweep_plane) may lie across the
+    // periodic z boundary: its global plane, cell id and cell centre are the owner's
+#ifndef PMC_NO_ZG_WRAP   // (A/B builds only: the wrap's cost on the whole-box kernel)
+    cg.zg0 += cg.zg0 < 0 ? g.cps_z : 0;
+    cg.zg0 -= cg.zg0 >= g.cps_z ? g.cps_z : 0;
+#endif
     const int plane = g.cps_x * g.cps_y;
     cg.c = (uint32_t)(cg.x + g.cps_x * cg.y + plane * (cg.zl + g.halo));
     cg.id = (uint32_t)cg.x + (uint32_t)g.cps_x * ((uint32_t)cg.y + (uint32_t)g.cps_y * (uint32_t)cg.zg0);
@@ -2541,6 +2547,21 @@ hipError_t launch_subsweep_boundary(const DevGeom& g, float* disk, const int16_t
     return hipGetLastError();
 }
 
+hipError_t launch_subsweep_plane(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
+                                 uint32_t sweep, unsigned long long* stats, int* ovf, int zl, hipStream_t st,
+                                 const LaunchTiming* tm) {
+    // one colour plane z = zl (parity oz) of storage, halo planes included (-halo .. nz_local-1+halo):
+    // the boundary launch's per-cell path (main capacity + fallback), colour plane cz = (zl - oz) / 2
+    if (((zl - oz) & 1) || zl < -g.halo || zl > g.nz_local - 1 + g.halo) return hipErrorInvalidValue;
+    // the visit reads planes zl - 1 .. zl + 1, which must be stored
+    if (g.halo && (zl - 1 < -g.halo || zl + 1 > g.nz_local - 1 + g.halo)) return hipErrorInvalidValue;
+    const int cz = (zl - oz) >> 1;   // arithmetic shift: floor, so zl = -1 (oz = 1) gives -1
+    const int64_t bytes = (int64_t)g.cps_x * g.cps_y * (g.nz_local + 2 * g.halo) * 3 * g.nmax * 4;
+    if (bytes < ((int64_t)1 << 32)) launch_direct_n<true>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz, 1, nullptr, 0, st, tm);
+    else launch_direct_n<false>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz, 1, nullptr, 0, st, tm);
+    return hipGetLastError();
+}
+
 hipError_t launch_subsweep(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
                            uint32_t sweep, unsigned long long* stats, int* ovf, int zl_begin, int zl_end,
                            hipStream_t st, const LaunchTiming* tm) {
@@ -2614,7 +2635,7 @@ hipError_t launch_shift_planes(const DevGeom& g, const float* din, const int16_t
     if (zl_begin < -g.halo || zl_end > g.nz_local + g.halo || zl_end <= zl_begin) return hipErrorInvalidValue;
     if (f == 2 && g.halo) {   // along z each plane reads its dir-neighbour, which must be stored
         const int dir = (d <= 0) ? -1 : 1;
-        if (zl_begin + dir < -1 || zl_end - 1 + dir > g.nz_local) return hipErrorInvalidValue;
+        if (zl_begin + dir < -g.halo || zl_end - 1 + dir > g.nz_local - 1 + g.halo) return hipErrorInvalidValue;
     }
 #ifndef PMC_SHIFT_U
 #define PMC_SHIFT_U 8

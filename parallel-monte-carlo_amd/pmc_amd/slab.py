@@ -402,28 +402,37 @@ class SlabDriver:
     runs of equal z parity; per run the interior planes go in 1-3 launch chains on their own streams
     (PMC_SLAB_CHAINS) and the run's boundary plane on the exchange stream, which then sends that whole
     plane to the neighbour holding it as a halo and receives the opposite halo (one RCCL send/recv
-    each way per run); after shiftCells only a z shift needs one more plane.  The host issues a sweep
-    in a few dozen HIP/RCCL calls.  SlabSimulation above is the older per-colour schedule in Python
+    each way per run); after shiftCells only a z shift needs one more plane.  With halo=2 (two halo
+    planes per side; PMC_SLAB_HALO=2 sets the default) the first run also visits the neighbour's
+    boundary plane redundantly and a sweep needs ONE exchange, after shiftCells.
+    The host issues a sweep in a few dozen HIP/RCCL calls.  SlabSimulation above is the older per-colour schedule in Python
     over torch.distributed; the CPU tests drive it with the oracle and gloo.
     """
 
     def __init__(self, cps: int, nz_local: int, rank: int, world: int, stream=None, atoms_per_rank: int = 0,
                  atoms_total: int = 0, nmax: int = 16, n_moves: int = 10, seed: int = 1234,
                  use_rccl: Optional[bool] = None, group=None, local_group=None, cps_y: int = 0,
-                 flags: int = 0, lattice_cps_z: int = 0):
+                 flags: int = 0, lattice_cps_z: int = 0, halo: int = 0):
         """local_group: a pmc_amd.engine.LocalGroup -- the in-process transport (this rank is one of
         local_group.world slab contexts of this process; construct and drive each rank from its
         own thread: the exchanges are collective).  flags: pmc_params.flags (PMC_FLAG_FULL_SHUFFLE:
         the reference-like colour order, up to 8 runs and exchanges per sweep).  lattice_cps_z with
         atoms_total: the lattice of atoms_total particles over a box lattice_cps_z cells tall
-        (pmc_init_lattice_planes; the config-5 weak-scaling start), else over this box."""
+        (pmc_init_lattice_planes; the config-5 weak-scaling start), else over this box.  halo: halo
+        planes per side, 1 or 2 (0: PMC_SLAB_HALO, default 1; the reference-like colour order always
+        uses 1)."""
         from .engine import PmcContext, comm_unique_id
         self.g = SlabGeometry(cps, nz_local, rank, world, nmax)
         if stream is None and local_group is None:
             import torch
             stream = torch.cuda.Stream()
         self.stream = stream
-        self.ctx = PmcContext(cps, cps_y=cps_y, cps_z=self.g.cps_z, nz_local=nz_local, z0=self.g.z0, halo=1,
+        if not halo:
+            halo = int(os.environ.get("PMC_SLAB_HALO", "1") or 1)
+        if flags & 1:            # PMC_FLAG_FULL_SHUFFLE: up to 8 runs a sweep, one-plane halos
+            halo = 1
+        self.halo = halo
+        self.ctx = PmcContext(cps, cps_y=cps_y, cps_z=self.g.cps_z, nz_local=nz_local, z0=self.g.z0, halo=halo,
                               nmax=nmax, n_moves=n_moves, seed=seed, flags=flags,
                               stream=stream.cuda_stream if stream is not None else None)
         self.cps_y = cps_y or cps
@@ -477,8 +486,9 @@ class SlabDriver:
         full_d, full_n = self.ctx.copy_out()
         plane = self.g.cps * self.cps_y
         row = 3 * self.g.nmax
-        full_d[plane * row:(self.g.nz + 1) * plane * row] = np.asarray(disk, np.float32).reshape(-1)
-        full_n[plane:(self.g.nz + 1) * plane] = np.asarray(n, np.int16).reshape(-1)
+        h = self.halo
+        full_d[h * plane * row:(self.g.nz + h) * plane * row] = np.asarray(disk, np.float32).reshape(-1)
+        full_n[h * plane:(self.g.nz + h) * plane] = np.asarray(n, np.int16).reshape(-1)
         self.ctx.copy_in(full_d, full_n)
         self.ctx.slab_exchange()
 
@@ -487,4 +497,5 @@ class SlabDriver:
         d, n = self.ctx.copy_out()
         plane = self.g.cps * self.cps_y
         row = 3 * self.g.nmax
-        return d[plane * row:(self.g.nz + 1) * plane * row], n[plane:(self.g.nz + 1) * plane]
+        h = self.halo
+        return d[h * plane * row:(self.g.nz + h) * plane * row], n[h * plane:(self.g.nz + h) * plane]

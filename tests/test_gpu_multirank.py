@@ -116,9 +116,10 @@ def test_c_slab_driver_world_equals_oracle(pmc, oracle, world, cps, cps_y, cps_z
     group.close()
 
 
-def test_c_slab_driver_world3_restart(pmc, oracle, tmp_path):
+@pytest.mark.parametrize("halo", [1, 2])
+def test_c_slab_driver_world3_restart(pmc, oracle, tmp_path, halo):
     """Per-rank snapshots + halo refill through the in-process transport: a fresh group restored
-    from the snapshots repeats the last sweeps bit for bit."""
+    from the snapshots repeats the last sweeps bit for bit (one- and two-plane halos)."""
     from pmc_amd.engine import LocalGroup
     from pmc_amd.slab import SlabDriver
     world, cps, cps_z, atoms = 3, 16, 12, 7_500
@@ -130,7 +131,7 @@ def test_c_slab_driver_world3_restart(pmc, oracle, tmp_path):
     keep = []
 
     def part1(r):
-        d = SlabDriver(cps=cps, nz_local=nz, rank=r, world=world, atoms_total=atoms, local_group=group)
+        d = SlabDriver(cps=cps, nz_local=nz, rank=r, world=world, atoms_total=atoms, local_group=group, halo=halo)
         keep.append(d)
         d.run(first, 3)
         d.ctx.save_snapshot(paths[r], first + 3)
@@ -145,7 +146,7 @@ def test_c_slab_driver_world3_restart(pmc, oracle, tmp_path):
     keep2 = []
 
     def part2(r):
-        d = SlabDriver(cps=cps, nz_local=nz, rank=r, world=world, local_group=group2)
+        d = SlabDriver(cps=cps, nz_local=nz, rank=r, world=world, local_group=group2, halo=halo)
         keep2.append(d)
         s = d.ctx.load_snapshot(paths[r])
         d.ctx.slab_exchange()
@@ -263,7 +264,7 @@ print("ok")
     assert "ok" in out.stdout
 
 
-def _world_vs_oracle(pmc, oracle, world, cps, nz, atoms, first, count, lattice_cps_z=0, threads=16):
+def _world_vs_oracle(pmc, oracle, world, cps, nz, atoms, first, count, lattice_cps_z=0, threads=16, halo=1):
     """World ranks of the C slab driver (in-process transport, one GPU) over `count` sweeps of the
     cps x cps x world*nz box against the oracle's whole-box run: every occupied slot, counts, the
     four counters (summed over ranks and through pmc_slab_observables) and the energy."""
@@ -275,7 +276,7 @@ def _world_vs_oracle(pmc, oracle, world, cps, nz, atoms, first, count, lattice_c
 
     def rank_main(r):
         d = SlabDriver(cps=cps, nz_local=nz, rank=r, world=world, atoms_total=atoms, local_group=group,
-                       lattice_cps_z=lattice_cps_z)
+                       lattice_cps_z=lattice_cps_z, halo=halo)
         drivers[r] = d
         d.run(first, count)
         d.ctx.synchronize()
@@ -321,6 +322,48 @@ def test_config4_world8_128_equals_oracle(pmc, oracle):
     plans = [oracle.sweep_plan(1234, s, 2.5) for s in (13, 14, 15)]
     assert {(f, d > 0) for _, f, d in plans} >= {(2, True), (2, False)}
     _world_vs_oracle(pmc, oracle, world=8, cps=128, nz=16, atoms=10_000_000, first=13, count=3)
+
+
+@pytest.mark.timeout(400)
+def test_config4_world8_128_halo2_equals_oracle(pmc, oracle):
+    """Config 4 at its workload with two-plane halos (one exchange per sweep, the neighbour's
+    boundary plane visited redundantly in the first run): sweeps 13-15, whose z shifts include the
+    case that exchanges the stale halo before shiftCells (sweep 13: first run parity 1, +z), bit for
+    bit against the oracle's whole box."""
+    _world_vs_oracle(pmc, oracle, world=8, cps=128, nz=16, atoms=10_000_000, first=13, count=3, halo=2)
+
+
+def _window_h2(oracle, count=8):
+    """First sweep of a window with shifts along x, y and z whose z shifts cover all four cases of
+    the two-plane-halo schedule: first-run parity a = 0 with dir < 0 and a = 1 with dir > 0 (the
+    halo shiftCells reads is stale: one plane exchanged first, T shifts the boundary plane) and the
+    two fresh ones."""
+    for s in range(0, 1000):
+        ks = []
+        for k in range(count):
+            o, f, d = oracle.sweep_plan(1234, s + k, 2.5)
+            ks.append((f, o[0] % 2, -1 if d <= 0 else 1))
+        z = {(a, dr) for f, a, dr in ks if f == 2}
+        if {f for f, _, _ in ks} == {0, 1, 2} and z == {(0, -1), (0, 1), (1, -1), (1, 1)}:
+            return s
+    raise AssertionError("no window")
+
+
+@pytest.mark.parametrize("world,cps,nz,atoms", [
+    (1, 32, 32, 120_000),      # one rank: the halos are its own planes (periodic)
+    (2, 16, 8, 10_000),
+    (3, 16, 4, 7_500),
+    (4, 32, 8, 120_000),
+    (8, 16, 2, 10_000),        # 2 planes per rank: the send planes are the whole slab
+])
+def test_c_slab_driver_halo2_equals_oracle(pmc, oracle, world, cps, nz, atoms):
+    """Two-plane halos (pmc_params.halo = 2, slab_sweep_h2) through the in-process transport over a
+    window of 8 sweeps with shifts along x, y and both z cases of each first-run parity, against the
+    oracle's whole box: every occupied slot, counts, the four counters (the redundant halo visits
+    count nowhere), the energy, no error flag."""
+    first = _window_h2(oracle)
+    o = _world_vs_oracle(pmc, oracle, world=world, cps=cps, nz=nz, atoms=atoms, first=first, count=8, halo=2)
+    assert o["evaluated"] > 0
 
 
 @pytest.mark.timeout(600)
