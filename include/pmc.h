@@ -45,7 +45,9 @@ typedef struct pmc_params {
     int32_t nz_local;   /* z-planes owned by this context (0 -> cps_z); even */
     int32_t z0;         /* global z index of the first owned plane; even */
     int32_t halo;       /* 0: storage holds the whole periodic box (nz_local == cps_z);
-                           1: slab mode, one halo plane below and above the owned planes */
+                           1: slab mode, one halo plane below and above the owned planes;
+                           2: slab mode with two halo planes per side (the slab driver's
+                              one-exchange-per-sweep schedule; needs the grouped colour order) */
     int32_t nmax;       /* particle slots per cell (nmax), 1..64 */
     int32_t n_moves;    /* trial moves per cell visit (n_M) */
     float w;            /* cell width == LJ cutoff rc (w); box L = cps * w */
@@ -174,7 +176,13 @@ int pmc_phase_range_on(pmc_ctx* ctx, int colour, uint32_t sweep, int zl_begin, i
  * After shiftCells only a z shift needs one more plane (with its counts) from one side.  Every rank
  * derives the sweep plan itself and RNG counters use global cell ids, so any world size
  * reproduces the single-GPU run bit for bit.  librccl is dlopen'ed ("librccl.so.1", or the path
- * in PMC_RCCL_LIB). */
+ * in PMC_RCCL_LIB).
+ * Contexts created with halo = 2 run a different schedule with ONE exchange per sweep: the first
+ * run also visits the neighbour's boundary plane of its parity (a halo plane) redundantly, on a
+ * stream of its own (its counters are not added: the owner counts them), so the second run needs no
+ * exchange; after shiftCells the four planes next to the slab's faces travel with their counts
+ * (and, for a z shift whose dir-side halo is the stale one, one plane before it).  Same results bit
+ * for bit; DESIGN.md section 6 has the measurements (slower than halo = 1 on one GPU). */
 /* rank 0: a fresh RCCL unique id (128 bytes) to broadcast to the other ranks */
 int pmc_comm_unique_id(unsigned char id[128]);
 /* Attach the slab driver: create the RCCL communicator (collective over the world ranks; id from
