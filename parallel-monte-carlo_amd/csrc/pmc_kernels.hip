@@ -2439,6 +2439,11 @@ int subsweep_capacity(const DevGeom& g) {
 }
 
 template <int NSLOT, int NMC, bool OFF32>
+static void launch_direct_t(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz, uint32_t sweep,
+                            unsigned long long* stats, int* ovf, int cz0, int ncz, float* mirror, int mode,
+                            hipStream_t st, const LaunchTiming* tm);
+
+template <int NSLOT, int NMC, bool OFF32>
 static void launch_subsweep_t(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
                               uint32_t sweep, unsigned long long* stats, int* ovf, int cz0, int ncz,
                               hipStream_t st, const LaunchTiming* tm) {
@@ -2452,6 +2457,14 @@ static void launch_subsweep_t(const DevGeom& g, float* disk, const int16_t* n, i
         const size_t lds_full = sizeof(float) * (size_t)lds_floats_per_wave(full) * kSubWaves;
         launch_k(k_subsweep_full<NSLOT, NMC, OFF32>, dim3((unsigned)((total + kSubWaves - 1) / kSubWaves)),
                  dim3(kWave * kSubWaves), lds_full, st, tm, g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz);
+        return;
+    }
+    // PMC_DIRECT_CELLS=<n> (default 0: off): phases of at most n cells as one cell per wave at the
+    // main capacity (the slab boundary launch's form) -- half-length waves, more of them, for phases
+    // of a few rounds of the chip's wave slots (A/B switch)
+    static const int64_t direct_cells = env_cells("PMC_DIRECT_CELLS", 0);
+    if (total <= direct_cells) {
+        launch_direct_t<NSLOT, NMC, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, nullptr, 0, st, tm);
         return;
     }
     size_t lds = sizeof(float) * (size_t)lds_floats_per_wave(kMainCap) * kSubWaves;

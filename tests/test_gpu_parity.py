@@ -518,17 +518,19 @@ def test_gpu_init_lattice_global_slab_planes(pmc, oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nz,atoms,rccl", [(16, 10_000, False), (16, 10_000, True), (4, 2_500, True)])
-def test_gpu_c_slab_driver_equals_whole_box(pmc, oracle, nz, atoms, rccl):
-    """The C slab driver (pmc_slab_*: two streams, colour-packed halo exchange; with rccl=True
-    through a one-rank RCCL communicator sending to itself, the multi-GPU transport path) equals
-    the whole-box run bit for bit: every occupied slot, counts, counters and the energy.
-    Sweeps 10-17 shift along x and y (10-12: both halo planes shifted locally) and along z in
-    both directions (13-17: one halo plane shifted locally, the other received); after the last
-    one both halo planes must equal the periodic images of the owned boundary planes."""
+@pytest.mark.parametrize("nz,atoms,rccl,halo", [(16, 10_000, False, 1), (16, 10_000, True, 1), (4, 2_500, True, 1),
+                                               (16, 10_000, True, 2), (4, 2_500, False, 2)])
+def test_gpu_c_slab_driver_equals_whole_box(pmc, oracle, nz, atoms, rccl, halo):
+    """The C slab driver (pmc_slab_*: interior chains, boundary chain with the halo exchange; with
+    rccl=True through a one-rank RCCL communicator sending to itself, the multi-GPU transport path;
+    halo=2: the one-exchange-per-sweep schedule with two halo planes per side) equals the whole-box
+    run and the C oracle's bit for bit: every occupied slot, counts, counters and the energy.
+    Sweeps 10-17 shift along x and y (10-12: the halo planes shifted locally) and along z in both
+    directions (13-17: one halo plane shifted locally, the other received); after the last one
+    every halo plane must equal the periodic image of its owned plane."""
     import torch
     from pmc_amd.slab import SlabDriver
-    drv = SlabDriver(cps=16, nz_local=nz, rank=0, world=1, atoms_per_rank=atoms, use_rccl=rccl)
+    drv = SlabDriver(cps=16, nz_local=nz, rank=0, world=1, atoms_per_rank=atoms, use_rccl=rccl, halo=halo)
     whole = pmc.PmcContext(16, cps_z=nz)
     whole.init_lattice(atoms)
     assert int(whole.copy_out()[1].sum()) == atoms, "whole box: lattice not binned"
@@ -542,18 +544,26 @@ def test_gpu_c_slab_driver_equals_whole_box(pmc, oracle, nz, atoms, rccl):
     assert int(n.sum()) == atoms, f"whole box: particles lost (sum {int(n.sum())}, stats {whole.stats()})"
     assert np.array_equal(n_slab, n)
     assert oracle.valid_slots_equal(d_slab, n_slab, disk, n, 16)
+    st = oracle.OracleState(oracle.make_params(cps=16, cps_z=nz))     # and the oracle's run itself
+    assert st.init_lattice(atoms) == 0
+    assert st.run(10, 8) == 0
+    assert np.array_equal(n_slab, st.n)
+    assert oracle.valid_slots_equal(d_slab, n_slab, st.disk, st.n, 16)
+    assert drv.ctx.stats() == st.stats.as_dict()
     d_all, n_all = drv.ctx.copy_out()
     plane, row = 16 * 16, 3 * 16
-    d_all = d_all.reshape(nz + 2, plane * row)
-    n_all = n_all.reshape(nz + 2, plane)
-    for halo, image in ((0, nz), (nz + 1, 1)):
-        assert np.array_equal(n_all[halo], n_all[image])
-        assert oracle.valid_slots_equal(d_all[halo], n_all[halo], d_all[image], n_all[image], 16)
+    d_all = d_all.reshape(nz + 2 * halo, plane * row)
+    n_all = n_all.reshape(nz + 2 * halo, plane)
+    for k in range(halo):   # storage plane of local z is z + halo
+        for hz, image in ((halo - 1 - k, halo + nz - 1 - k), (halo + nz + k, halo + k)):
+            assert np.array_equal(n_all[hz], n_all[image])
+            assert oracle.valid_slots_equal(d_all[hz], n_all[hz], d_all[image], n_all[image], 16)
     assert drv.ctx.stats() == whole.stats()
     assert drv.ctx.error_flags() == 0
     assert drv.ctx.energy() == pytest.approx(whole.energy(), rel=1e-12, abs=1e-9)
     obs, e_all = drv.ctx.slab_observables()   # one rank: the RCCL all-reduce (or local) of itself
     assert obs == whole.stats() and e_all == whole.energy()
+    assert e_all == st.energy()
 
 
 @pytest.mark.gpu
