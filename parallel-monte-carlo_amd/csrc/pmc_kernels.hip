@@ -198,6 +198,40 @@ __device__ __forceinline__ pmc_u32x4 philox_sched(uint32_t c0, uint32_t c1, uint
     return out;
 }
 
+// The same Philox with the round keys formed on the fly from (k0, k1) -- for the RARE paths inside
+// a visit (moves beyond the first chunk, more than 16 own particles).  The key words are laundered
+// through an empty asm in the rare block itself, so the compiler cannot hoist the schedule out of
+// it: the 20 round-key SGPRs of philox_sched then need not stay live across the move loop, where
+// they pushed other loop values into SGPR spills (v_writelane / v_readlane per move).
+#ifndef PMC_RARE_KEYS
+#define PMC_RARE_KEYS 1
+#endif
+__device__ __forceinline__ pmc_u32x4 philox_rare(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                                 const DevGeom& g) {
+#if PMC_RARE_KEYS
+    uint32_t k0 = g.k0, k1 = g.k1;
+    asm volatile("" : "+s"(k0), "+s"(k1));
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)PMC_PHILOX_M0 * (uint64_t)c0;
+        const uint64_t p1 = (uint64_t)PMC_PHILOX_M1 * (uint64_t)c2;
+        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c1 = (uint32_t)p1;
+        c3 = (uint32_t)p0;
+        c0 = n0;
+        c2 = n2;
+        k0 += PMC_PHILOX_W0;
+        k1 += PMC_PHILOX_W1;
+    }
+    pmc_u32x4 out;
+    out.v[0] = c0; out.v[1] = c1; out.v[2] = c2; out.v[3] = c3;
+    return out;
+#else
+    return philox_sched(c0, c1, c2, c3, g);
+#endif
+}
+
 // exact n / d for 32-bit n (Granlund-Montgomery round-up method; magic from make_udiv_magic)
 __device__ __forceinline__ uint32_t udiv_magic(uint32_t n, UDivMagic m) {
     const uint32_t hi = __umulhi(n, m.mul);
@@ -434,7 +468,7 @@ __device__ __forceinline__ void rng_chunk_single(const DevGeom& g, uint32_t id, 
     const int lane = threadIdx.x & (kWave - 1);
     const int j = lane & 15;
     const uint32_t tag = (lane & 48) == 16 ? PMC_TAG_ACCEPT : PMC_TAG_MOVE;
-    const pmc_u32x4 w = philox_sched((uint32_t)(m0 + j), id, sweep, tag, g);
+    const pmc_u32x4 w = philox_rare((uint32_t)(m0 + j), id, sweep, tag, g);
     const uint32_t wl = lane < 32 ? w.v[0] : w.v[2];
     const uint32_t ws = lane < 32 ? w.v[1] : w.v[3];
     const float lg = pmc_logf(pmc_u01(wl));
@@ -452,7 +486,7 @@ __device__ __forceinline__ void rng_chunk_single(const DevGeom& g, uint32_t id, 
 // 4 words through LDS scratch `tmp` (64 floats; the term list area, free outside the moves).
 __device__ __forceinline__ int fy_words_single(const DevGeom& g, uint32_t id, uint32_t sweep, float* tmp) {
     const int lane = threadIdx.x & (kWave - 1);
-    const pmc_u32x4 w = philox_sched((uint32_t)(lane & 15), id, sweep, PMC_TAG_SHUFFLE, g);
+    const pmc_u32x4 w = philox_rare((uint32_t)(lane & 15), id, sweep, PMC_TAG_SHUFFLE, g);
     if (lane < 16) *(uint4*)(tmp + 4 * lane) = make_uint4(w.v[0], w.v[1], w.v[2], w.v[3]);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     const uint32_t wi = *(const uint32_t*)(tmp + lane);
