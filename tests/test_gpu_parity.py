@@ -657,3 +657,18 @@ def test_timing_pause_samples_launches(pmc):
     ctx.sweep(4)
     k = ctx.timing_kinds(False)
     assert k["n_subsweep"] == 8 and k["n_shift"] == 1
+
+
+@pytest.mark.gpu
+def test_slab_halo_parameter_validation(pmc):
+    """pmc_params.halo: 0 (whole box), 1 or 2 (slabs); 2 refuses the reference-like colour order (its
+    schedule needs two runs per sweep), other values are refused; a two-plane-halo context stores
+    nz_local + 4 planes and its plane spans reach the outer halos."""
+    with pytest.raises(pmc.PmcError, match="halo must be"):
+        pmc.PmcContext(16, cps_z=16, nz_local=8, z0=0, halo=3)
+    with pytest.raises(pmc.PmcError, match="two runs per sweep"):
+        pmc.PmcContext(16, cps_z=16, nz_local=8, z0=0, halo=2, flags=1)
+    ctx = pmc.PmcContext(16, cps_z=16, nz_local=8, z0=8, halo=2)
+    d, n = ctx.copy_out()
+    assert n.size == 16 * 16 * (8 + 4)
+    ctx.close()
