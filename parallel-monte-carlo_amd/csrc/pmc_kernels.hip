@@ -206,6 +206,9 @@ __device__ __forceinline__ pmc_u32x4 philox_sched(uint32_t c0, uint32_t c1, uint
 #ifndef PMC_RARE_KEYS
 #define PMC_RARE_KEYS 1
 #endif
+#ifndef PMC_HALF_BLOCK
+#define PMC_HALF_BLOCK 0   // (A/B switch, measured slower) the last partner block in one pass when <= 32
+#endif
 __device__ __forceinline__ pmc_u32x4 philox_rare(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                                  const DevGeom& g) {
 #if PMC_RARE_KEYS
@@ -684,6 +687,12 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
     // block code with no per-move loop or bound tests (the full-capacity launches keep the loop).
     auto move_loop = [&](auto nb_c) {
     constexpr int NB = decltype(nb_c)::value;
+#if PMC_HALF_BLOCK
+    // the last 64-partner block holds at most 32 partners (about half the cells at 4.77 per cell:
+    // K ~ 98): its new and old positions share one pass (below)
+    const bool half_last = NB > 0 && K - (NB - 1) * kWave <= 32;
+    const uint32_t hsgn = (uint32_t)(lane & 32) << 26;   // lanes 32-63: the sign bit (old terms)
+#endif
     unsigned long long pend = 0;                       // in-cell moves of the current round
     int sp_l = 0;                                      // lane j: row slot of the round's move j
 #ifdef PMC_PROBE_NO_REPEAT_OLD
@@ -780,7 +789,29 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
                 };
                 if constexpr (NB > 0) {
 #pragma unroll
-                    for (int b = 0; b < NB; ++b) block(b * kWave, b == 0 ? sbit : 0ull);
+                    for (int b = 0; b < NB - 1; ++b) block(b * kWave, b == 0 ? sbit : 0ull);
+                    const unsigned long long xl = NB == 1 ? sbit : 0ull;   // the moving slot (block 0)
+#if PMC_HALF_BLOCK
+                    if (half_last) {
+                        // the last block holds at most 32 partners: new (lanes 0-31) and old (lanes
+                        // 32-63) positions of partners base + (lane & 31) in ONE pass -- one r2, one
+                        // compare, one ballot + mbcnt, one store.  Ballot order is lane order, so the
+                        // list is the two-pass one exactly: the block's new terms ascending, then its
+                        // old terms ascending, as -r2 (the sign bit: pmc_r2_neg is -pmc_r2 bit for
+                        // bit, and -r2 >= -rc2 is r2 <= rc2)
+                        const float hx = lane < 32 ? qx : xi, hy = lane < 32 ? qy : yi, hz = lane < 32 ? qz : zi;
+                        const int k = (NB - 1) * kWave + (lane & 31);
+                        const float xj = px_[k], yj = py_[k], zj = pz_[k];
+                        const float r2 = pmc_r2(hx - xj, hy - yj, hz - zj);
+                        const unsigned long long m = __builtin_amdgcn_ballot_w64(r2 <= rc2) & ~(xl | (xl << 32));
+                        if (__builtin_amdgcn_inverse_ballot_w64(m)) buf[mbcnt64_add(m, C)] = as_f(as_i(r2) | hsgn);
+                        C += __popcll(m);
+                    } else {
+                        block((NB - 1) * kWave, xl);
+                    }
+#else
+                    block((NB - 1) * kWave, xl);
+#endif
                 } else {
                     block(0, sbit);
                     for (int base = kWave; base < K; base += kWave) block(base, 0ull);
