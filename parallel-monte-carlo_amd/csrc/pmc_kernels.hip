@@ -1517,7 +1517,10 @@ __device__ __forceinline__ void shift_store(float* p, float v) {
 #endif
 }
 
-template <int NSLOT, int U>
+// OFF32 (buffer < 4 GiB, PMC_SHIFT_OFF32=1): 32-bit byte offsets from the SGPR bases (global_load /
+// store with a VGPR offset), else 64-bit element addressing (default: the 32-bit form saves 170
+// address instructions and 27 VGPRs but not time, profiles/r04_shift_counters.json)
+template <int NSLOT, int U, int OFF32>
 __global__ __launch_bounds__(kShiftThreads) void k_shift(DevGeom g, const float* __restrict__ din,
                                                const int16_t* __restrict__ nin, float* __restrict__ dout,
                                                int16_t* __restrict__ nout, int f, float d,
@@ -1597,17 +1600,28 @@ __global__ __launch_bounds__(kShiftThreads) void k_shift(DevGeom g, const float*
         const uint32_t cnb = (uint32_t)nx + (uint32_t)g.cps_x * (uint32_t)ny + plane * (uint32_t)(nz + g.halo);
         // one round trip: both counts and all six rows (a 64 B row sits inside one 128 B line)
         // unconditional loads (c, cnb are valid cells for dead lanes too: no branch, no wait)
-        const int nc0 = nin[c[j]], nn0 = nin[cnb];
+        const int nc0 = OFF32 ? *(const int16_t*)((const char*)nin + (uint64_t)(c[j] * 2u)) : nin[c[j]];
+        const int nn0 = OFF32 ? *(const int16_t*)((const char*)nin + (uint64_t)(cnb * 2u)) : nin[cnb];
         ncur[j] = live[j] ? nc0 : 0;
         nnb[j] = live[j] ? nn0 : 0;
         cnbv[j] = cnb;
 #ifndef PMC_SHIFT_MASKED
-        const uint64_t oc = (uint64_t)c[j] * (uint64_t)(3 * nm) + (uint64_t)pp;
-        const uint64_t on = (uint64_t)cnb * (uint64_t)(3 * nm) + (uint64_t)pp;
+        if constexpr (OFF32) {
+            const uint32_t oc = (c[j] * (uint32_t)(3 * nm) + (uint32_t)pp) * 4u;
+            const uint32_t on = (cnb * (uint32_t)(3 * nm) + (uint32_t)pp) * 4u;
 #pragma unroll
-        for (int dim = 0; dim < 3; ++dim) {
-            own[j][dim] = din[oc + (uint64_t)(dim * nm)];
-            nbv[j][dim] = din[on + (uint64_t)(dim * nm)];
+            for (int dim = 0; dim < 3; ++dim) {
+                own[j][dim] = DiskAddr<1>::ld(din, oc + (uint32_t)(dim * nm) * 4u);
+                nbv[j][dim] = DiskAddr<1>::ld(din, on + (uint32_t)(dim * nm) * 4u);
+            }
+        } else {
+            const uint64_t oc = (uint64_t)c[j] * (uint64_t)(3 * nm) + (uint64_t)pp;
+            const uint64_t on = (uint64_t)cnb * (uint64_t)(3 * nm) + (uint64_t)pp;
+#pragma unroll
+            for (int dim = 0; dim < 3; ++dim) {
+                own[j][dim] = din[oc + (uint64_t)(dim * nm)];
+                nbv[j][dim] = din[on + (uint64_t)(dim * nm)];
+            }
         }
 #endif
     }
@@ -1636,13 +1650,19 @@ __global__ __launch_bounds__(kShiftThreads) void k_shift(DevGeom g, const float*
         const unsigned long long tm = (__ballot(take) >> gsh) & gmask;
         const int nk = __popcll(km);
         const int nnew = nk + __popcll(tm);
-        const uint64_t ob = (uint64_t)c[j] * (uint64_t)(3 * nm);
+        // output slot `dst` of dimension row `dim` of cell c[j]: element offset c*3nm + dim*nm + dst
+        auto out_at = [&](int dim, int dst) -> float* {
+            if constexpr (OFF32)
+                return (float*)((char*)dout + (uint64_t)((c[j] * (uint32_t)(3 * nm) + (uint32_t)(dim * nm + dst)) * 4u));
+            else
+                return dout + (uint64_t)c[j] * (uint64_t)(3 * nm) + (uint64_t)(dim * nm + dst);
+        };
         if (keep) {
             const int dst = __popcll(km & below);
             if (dst < nm) {
 #pragma unroll
                 for (int dim = 0; dim < 3; ++dim)
-                    shift_store(dout + ob + (uint64_t)(dim * nm + dst), (dim == f) ? D + offset[j] : own[j][dim]);
+                    shift_store(out_at(dim, dst), (dim == f) ? D + offset[j] : own[j][dim]);
             }
         }
         if (take) {
@@ -1650,11 +1670,14 @@ __global__ __launch_bounds__(kShiftThreads) void k_shift(DevGeom g, const float*
             if (dst < nm) {
 #pragma unroll
                 for (int dim = 0; dim < 3; ++dim)
-                    shift_store(dout + ob + (uint64_t)(dim * nm + dst), (dim == f) ? ((Dn + offset[j]) + s) : nbv[j][dim]);   // own offset (VS shiftCells.h:96)
+                    shift_store(out_at(dim, dst), (dim == f) ? ((Dn + offset[j]) + s) : nbv[j][dim]);   // own offset (VS shiftCells.h:96)
             }
         }
         if (live[j] && p == 0) {
-            nout[c[j]] = (int16_t)(nnew > nm ? nm : nnew);
+            if constexpr (OFF32)
+                *(int16_t*)((char*)nout + (uint64_t)(c[j] * 2u)) = (int16_t)(nnew > nm ? nm : nnew);
+            else
+                nout[c[j]] = (int16_t)(nnew > nm ? nm : nnew);
             if (nnew > nm) atomicOr(flags, 1u);
         }
     }
@@ -2733,11 +2756,23 @@ hipError_t launch_shift_planes(const DevGeom& g, const float* din, const int16_t
     const dim3 block(kShiftThreads);
 #endif
     const int z0 = zl_begin;
+    // PMC_SHIFT_OFF32=1: 32-bit byte offsets when the storage is below 4 GiB (103 VGPRs, 4 waves per
+    // SIMD, -10% VALU) -- measured no faster (0.203-0.204 against 0.199-0.203 ms,
+    // profiles/r04q_shift_off32_ab.txt): the launch is bound by its DRAM bursts, not by issue or
+    // occupancy, so the 64-bit form stays the default
+    static const bool off32_env = env_cells("PMC_SHIFT_OFF32", 0) != 0;
+    const int64_t bytes = (int64_t)g.cps_x * g.cps_y * (g.nz_local + 2 * g.halo) * 3 * g.nmax * 4;
+    const bool off32 = off32_env && bytes < ((int64_t)1 << 32);
+    auto go = [&](auto ns) {
+        constexpr int NS = decltype(ns)::value;
+        if (off32) launch_k(k_shift<NS, U, 1>, grid, block, 0, st, tm, g, din, nin, dout, nout, f, d, flags, z0);
+        else launch_k(k_shift<NS, U, 0>, grid, block, 0, st, tm, g, din, nin, dout, nout, f, d, flags, z0);
+    };
     switch (g.nslot) {
-        case 8: launch_k(k_shift<8, U>, grid, block, 0, st, tm, g, din, nin, dout, nout, f, d, flags, z0); break;
-        case 16: launch_k(k_shift<16, U>, grid, block, 0, st, tm, g, din, nin, dout, nout, f, d, flags, z0); break;
-        case 32: launch_k(k_shift<32, U>, grid, block, 0, st, tm, g, din, nin, dout, nout, f, d, flags, z0); break;
-        default: launch_k(k_shift<64, U>, grid, block, 0, st, tm, g, din, nin, dout, nout, f, d, flags, z0); break;
+        case 8: go(std::integral_constant<int, 8>{}); break;
+        case 16: go(std::integral_constant<int, 16>{}); break;
+        case 32: go(std::integral_constant<int, 32>{}); break;
+        default: go(std::integral_constant<int, 64>{}); break;
     }
     return hipGetLastError();
 }
