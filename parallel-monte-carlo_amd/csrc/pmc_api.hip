@@ -1746,7 +1746,13 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
             const int zb = q == 0 ? 0 : nz - 1;
             int r;
             if (!first && (r = border_waits(kB, zb, zb + 1, q, T, p))) return r;
-            if ((r = phases(T, c->ovf_b, zb, zb + 1, k, k1, true))) return r;
+            // PMC_PROBE_SKIP_B=1: timing probe only (wrong results) -- the boundary chain's phase
+            // launches left out, the exchanges kept: what the boundary launches cost a rank sweep
+            static const bool skip_b = [] {
+                const char* v = std::getenv("PMC_PROBE_SKIP_B");
+                return v && std::atoi(v) == 1;
+            }();
+            if (!skip_b && (r = phases(T, c->ovf_b, zb, zb + 1, k, k1, true))) return r;
             PMC_HIP(hipEventRecord(s->ev_run[kB][q], T));
             if ((r = slab_exchange_run(c, q, merge_z))) return r;
             merge_z = false;
