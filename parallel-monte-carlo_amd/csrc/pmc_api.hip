@@ -251,7 +251,9 @@ int pmc_create(const pmc_params* params, pmc_ctx** out) {
         return cleanup(hip_fail(e, "hipMalloc eacc"));
     if ((e = hipMalloc(&c->flags, 16)) != hipSuccess) return cleanup(hip_fail(e, "hipMalloc flags"));
     {
-        const size_t per_colour = (size_t)(p.cps_x / 2) * (p.cps_y / 2) * (p.nz_local / 2);
+        // (at least two colour planes: a two-plane boundary launch, launch_subsweep_planes2, queues
+        // cells of two planes even when the slab has only one colour plane per parity)
+        const size_t per_colour = (size_t)(p.cps_x / 2) * (p.cps_y / 2) * (size_t)(p.nz_local / 2 > 2 ? p.nz_local / 2 : 2);
         // header (queue length, done counter: zero between launches) + one entry per cell
         const size_t ob = sizeof(int) * (kOvfHead + per_colour);
         if ((e = hipMalloc(&c->ovf, ob)) != hipSuccess) return cleanup(hip_fail(e, "hipMalloc ovf"));
@@ -1557,12 +1559,35 @@ int slab_sweep_h2(pmc_ctx* c, uint32_t sweep) {
         return PMC_OK;
     };
     int rc;
+    // PMC_SLAB_H2_MERGE (default 1): the boundary plane and the redundant halo plane of run a as ONE
+    // launch per phase on T (k_subsweep_direct2: the two planes lie at opposite faces), no R stream;
+    // 0: the halo plane on its own stream R
+    static const bool merge = [] {
+        const char* v = std::getenv("PMC_SLAB_H2_MERGE");
+        return !(v && std::atoi(v) == 0);
+    }();
     // ---- run a: T the boundary plane, R the halo plane of parity a, the interior chains --------
-    if ((rc = phases(T, c->ovf_b, c->stats, pa, pa + 1, 0, 4, true))) return rc;
-    PMC_HIP(hipEventRecord(s->ev_run[kB][a], T));
-    PMC_HIP(hipStreamWaitEvent(R, s->ev_x, 0));         // the last exchange filled the halos R reads
-    if ((rc = phases(R, c->ovf_aux2, s->stats_scratch, za, za + 1, 0, 4, true))) return rc;
-    PMC_HIP(hipEventRecord(s->ev_run[kR][a], R));
+    if (merge) {
+        const int z0 = pa < za ? pa : za, z1 = pa < za ? za : pa;
+        unsigned long long* s0 = z0 == pa ? c->stats : s->stats_scratch;
+        unsigned long long* s1 = z0 == pa ? s->stats_scratch : c->stats;
+        for (int kk = 0; kk < 4; ++kk) {
+            int o[3];
+            pmc_colour_offset(plan.order[kk], o);
+            LaunchTiming lt;
+            hipError_t le = launch_subsweep_planes2(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep, s0, s1,
+                                                    c->ovf_b, z0, z1, T, next_timing(c, 2, &lt));
+            if (le != hipSuccess) return hip_fail(le, "subsweep launch (two planes)");
+        }
+        PMC_HIP(hipEventRecord(s->ev_run[kB][a], T));
+        PMC_HIP(hipEventRecord(s->ev_run[kR][a], T));      // (the halo plane is T's too)
+    } else {
+        if ((rc = phases(T, c->ovf_b, c->stats, pa, pa + 1, 0, 4, true))) return rc;
+        PMC_HIP(hipEventRecord(s->ev_run[kB][a], T));
+        PMC_HIP(hipStreamWaitEvent(R, s->ev_x, 0));     // the last exchange filled the halos R reads
+        if ((rc = phases(R, c->ovf_aux2, s->stats_scratch, za, za + 1, 0, 4, true))) return rc;
+        PMC_HIP(hipEventRecord(s->ev_run[kR][a], R));
+    }
     for (int j = 0; j < nc; ++j) {
         if (zs[j + 1] > zs[j] && (rc = phases(ist[j], iovf[j], c->stats, zs[j], zs[j + 1], 0, 4, false))) return rc;
         PMC_HIP(hipEventRecord(s->ev_run[j][a], ist[j]));

@@ -96,6 +96,12 @@ hipError_t launch_subsweep_boundary(const DevGeom& g, float* disk, const int16_t
 hipError_t launch_subsweep_plane(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
                                  uint32_t sweep, unsigned long long* stats, int* ovf, int zl, hipStream_t st,
                                  const LaunchTiming* tm = nullptr);
+// two colour planes zl0 < zl1 of one parity in ONE launch (the two-plane-halo schedule's first run:
+// the boundary plane and the halo plane at the opposite face); plane zl0's counters to stats0, zl1's
+// to stats1
+hipError_t launch_subsweep_planes2(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
+                                   uint32_t sweep, unsigned long long* stats0, unsigned long long* stats1, int* ovf,
+                                   int zl0, int zl1, hipStream_t st, const LaunchTiming* tm = nullptr);
 int subsweep_capacity(const DevGeom& g);
 // whole sweeps of a small whole box in one launch on XCD 0 (k_sweep_small); bar: one unsigned of
 // scratch; cur: the current buffer of the (disk, n) pairs; returns hipErrorInvalidValue when the box

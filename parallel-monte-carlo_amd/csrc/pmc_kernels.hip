@@ -334,7 +334,7 @@ struct CellGeo {
 // With zlog, a range whose colour-plane count ncz the group size does not divide ends in a short
 // group of ncz % G planes (same order inside it: x, then its planes, then y).
 __device__ __forceinline__ CellGeo cell_geo(const DevGeom& g, int p, int cz0, int ox, int oy, int oz,
-                                            int zlog = 0, int ncz = 0) {
+                                            int zlog = 0, int ncz = 0, int czs = 1) {
     CellGeo cg;
     const int hx = g.cps_x >> 1, hy = g.cps_y >> 1;
     const uint32_t q1 = udiv_magic((uint32_t)p, g.div_ncx);     // p / hx: row of the visiting order
@@ -343,7 +343,7 @@ __device__ __forceinline__ CellGeo cell_geo(const DevGeom& g, int p, int cz0, in
     if (zlog == 0) {
         const uint32_t q2 = udiv_magic(q1, g.div_ncy);           // plane
         cg.tb = (int)q1 - (int)q2 * hy;
-        tcr = (int)q2;
+        tcr = (int)q2 * czs;                                     // (czs: colour planes czs apart)
     } else {
         const uint32_t lim = (uint32_t)(ncz >> zlog) * (uint32_t)hy << zlog;   // rows of the full groups
         if (q1 < lim) {
@@ -937,7 +937,7 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
                                               uint32_t sweep, unsigned long long* __restrict__ stats,
                                               float* __restrict__ px_, int lcap_rt, int cap, int t,
                                               int cz0, float* __restrict__ mirror = nullptr,
-                                              int mirror_mode = 0) {
+                                              int mirror_mode = 0, int czs = 1) {
     const int lane = threadIdx.x & (kWave - 1);
     const int nm = NMC > 0 ? NMC : g.nmax;
     const int lcap = LCAP > 0 ? LCAP : lcap_rt;
@@ -946,7 +946,7 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     float* py_ = px_ + stride;
     float* pz_ = py_ + stride;
     float* buf = pz_ + stride;
-    const CellGeo cg = cell_geo(g, t, cz0, ox, oy, oz);
+    const CellGeo cg = cell_geo(g, t, cz0, ox, oy, oz, 0, 0, czs);
     PMC_STAMP(0);
     const StencilLane sl = stencil_lane(g, cg, lane, cg.edge);
     const int k_cnt = ncnt[sl.kc];
@@ -1138,6 +1138,30 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_direct(DevGeom g
     if (!ok && (threadIdx.x & (kWave - 1)) == 0) ovf[kOvfHead + atomicAdd(&ovf[kOvfCount], 1)] = t;
 }
 
+// Two colour planes czs apart in ONE boundary launch (the two-plane-halo schedule's first run: the
+// boundary plane and the halo plane the neighbour owns, at opposite faces of the slab, so they never
+// interact): one cell per wave at the main capacity, cells of plane 0 of the pair first; each plane's
+// counters go to its own buffer (the redundant halo plane's to a scratch buffer).  Overflowing cells
+// are queued for k_subsweep_fallback2.
+template <int NSLOT, int NMC, bool OFF32>
+__global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_direct2(DevGeom g, float* __restrict__ disk,
+                                                                          const int16_t* __restrict__ ncnt,
+                                                                          int ox, int oy, int oz, uint32_t sweep,
+                                                                          unsigned long long* __restrict__ stats0,
+                                                                          unsigned long long* __restrict__ stats1,
+                                                                          int cap, int* __restrict__ ovf, int cz0, int czs) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float* px_ = smem + wv * lds_floats_per_wave(kMainCap);
+    const int per_plane = (g.cps_x >> 1) * (g.cps_y >> 1);
+    const int t = (int)blockIdx.x * kSubWaves + wv;
+    if (t >= 2 * per_plane) return;
+    unsigned long long* st = t < per_plane ? stats0 : stats1;
+    const bool ok = subsweep_wave<NSLOT, NMC, kMainCap, OFF32, false, PMC_BOUNDARY_PB>(
+        g, disk, ncnt, ox, oy, oz, sweep, st, px_, kMainCap, cap, t, cz0, nullptr, 0, czs);
+    if (!ok && (threadIdx.x & (kWave - 1)) == 0) ovf[kOvfHead + atomicAdd(&ovf[kOvfCount], 1)] = t;
+}
+
 // Fallback launch: full capacity (27*nmax partners per wave), a fixed grid striding over the
 // queued cells.  Cells of one colour are independent, so the order does not matter.
 template <int NSLOT, int NMC, bool OFF32, bool MIRROR = false>
@@ -1146,11 +1170,14 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_fallback(DevGeom
                                                                            int ox, int oy, int oz, uint32_t sweep,
                                                                            unsigned long long* __restrict__ stats,
                                                                            int* __restrict__ ovf, int cz0,
-                                                                           float* __restrict__ mirror = nullptr,
-                                                                           int mirror_mode = 0) {
+                                                                           float* __restrict__ mirror, int mirror_mode,
+                                                                           int czs, unsigned long long* __restrict__ stats1) {
+    // czs > 1: the queue of a two-plane launch (k_subsweep_direct2): planes czs apart, the second
+    // plane's counters to stats1
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int full = 27 * (NMC > 0 ? NMC : g.nmax);
+    const int per_plane = (g.cps_x >> 1) * (g.cps_y >> 1);
     float* px_ = smem + wv * lds_floats_per_wave(full);
     const int count = __builtin_amdgcn_readfirstlane(ovf[kOvfCount]);
     // nothing queued (the common case): nothing to clear either -- every workgroup reads the same
@@ -1159,8 +1186,9 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_fallback(DevGeom
     if (count == 0) return;
     for (int e = (int)blockIdx.x * kSubWaves + wv; e < count; e += (int)gridDim.x * kSubWaves) {
         const int t = __builtin_amdgcn_readfirstlane(ovf[kOvfHead + e]);
-        (void)subsweep_wave<NSLOT, NMC, 27 * NMC, OFF32, MIRROR>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, full,
-                                                                 full, t, cz0, mirror, mirror_mode);
+        unsigned long long* st = (czs != 1 && t >= per_plane) ? stats1 : stats;
+        (void)subsweep_wave<NSLOT, NMC, 27 * NMC, OFF32, MIRROR>(g, disk, ncnt, ox, oy, oz, sweep, st, px_, full,
+                                                                 full, t, cz0, mirror, mirror_mode, czs);
     }
     // the queue is cleared for the next launch (no memset between launches; graph replays start
     // from a clean queue): a one-workgroup grid clears it itself; otherwise the last workgroup to
@@ -2568,7 +2596,7 @@ static void launch_subsweep_t(const DevGeom& g, float* disk, const int16_t* n, i
 #endif
         const size_t lds_full = sizeof(float) * (size_t)lds_floats_per_wave(full) * kSubWaves;
         hipLaunchKernelGGL((k_subsweep_fallback<NSLOT, NMC, OFF32>), dim3(fallback_blocks()), dim3(kWave * kSubWaves), lds_full, st,
-                           g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0);
+                           g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, (float*)nullptr, 0, 1, stats);
     }
 }
 
@@ -2603,11 +2631,11 @@ static void launch_direct_t(const DevGeom& g, float* disk, const int16_t* n, int
         if (mirror)
             hipLaunchKernelGGL((k_subsweep_fallback<NSLOT, NMC, OFF32, true>), dim3(fallback_blocks()),
                                dim3(kWave * kSubWaves), lds_full, st, g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0,
-                               mirror, mode);
+                               mirror, mode, 1, stats);
         else
             hipLaunchKernelGGL((k_subsweep_fallback<NSLOT, NMC, OFF32>), dim3(fallback_blocks()),
                                dim3(kWave * kSubWaves), lds_full, st, g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0,
-                               nullptr, 0);
+                               (float*)nullptr, 0, 1, stats);
     }
 }
 
@@ -2645,6 +2673,48 @@ hipError_t launch_subsweep_boundary(const DevGeom& g, float* disk, const int16_t
     const int64_t bytes = (int64_t)g.cps_x * g.cps_y * (g.nz_local + 2 * g.halo) * 3 * g.nmax * 4;
     if (bytes < ((int64_t)1 << 32)) launch_direct_n<true>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, cz1 - cz0, mirror, mirror_mode, st, tm);
     else launch_direct_n<false>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, cz1 - cz0, mirror, mirror_mode, st, tm);
+    return hipGetLastError();
+}
+
+template <int NSLOT, int NMC, bool OFF32>
+static void launch_direct2_t(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz, uint32_t sweep,
+                             unsigned long long* stats0, unsigned long long* stats1, int* ovf, int cz0, int czs,
+                             hipStream_t st, const LaunchTiming* tm) {
+    const int64_t total = 2 * (int64_t)(g.cps_x / 2) * (g.cps_y / 2);
+    const int64_t blocks = (total + kSubWaves - 1) / kSubWaves;
+    const int cap = subsweep_capacity(g);
+    const int full = 27 * g.nmax;
+    const size_t lds = sizeof(float) * (size_t)lds_floats_per_wave(kMainCap) * kSubWaves;
+    launch_k(k_subsweep_direct2<NSLOT, NMC, OFF32>, dim3((unsigned)blocks), dim3(kWave * kSubWaves), lds, st, tm, g,
+             disk, n, ox, oy, oz, sweep, stats0, stats1, cap, ovf, cz0, czs);
+    if (cap < full) {
+        const size_t lds_full = sizeof(float) * (size_t)lds_floats_per_wave(full) * kSubWaves;
+        hipLaunchKernelGGL((k_subsweep_fallback<NSLOT, NMC, OFF32>), dim3(fallback_blocks()), dim3(kWave * kSubWaves),
+                           lds_full, st, g, disk, n, ox, oy, oz, sweep, stats0, ovf, cz0, (float*)nullptr, 0, czs, stats1);
+    }
+}
+
+hipError_t launch_subsweep_planes2(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
+                                   uint32_t sweep, unsigned long long* stats0, unsigned long long* stats1, int* ovf,
+                                   int zl0, int zl1, hipStream_t st, const LaunchTiming* tm) {
+    // planes zl0 < zl1 of colour parity oz (halo planes included), at least one plane apart
+    if (zl1 <= zl0 + 1 || ((zl0 - oz) & 1) || ((zl1 - oz) & 1)) return hipErrorInvalidValue;
+    for (int zl : {zl0, zl1})
+        if (zl - 1 < -g.halo || zl + 1 > g.nz_local - 1 + g.halo) return hipErrorInvalidValue;
+    const int cz0 = (zl0 - oz) >> 1, czs = (zl1 - zl0) >> 1;
+    const int64_t bytes = (int64_t)g.cps_x * g.cps_y * (g.nz_local + 2 * g.halo) * 3 * g.nmax * 4;
+    const bool off32 = bytes < ((int64_t)1 << 32);
+    auto go = [&](auto off) {
+        constexpr bool O = decltype(off)::value;
+        if (g.nmax == 16) launch_direct2_t<16, 16, O>(g, disk, n, ox, oy, oz, sweep, stats0, stats1, ovf, cz0, czs, st, tm);
+        else if (g.nmax == 32) launch_direct2_t<32, 32, O>(g, disk, n, ox, oy, oz, sweep, stats0, stats1, ovf, cz0, czs, st, tm);
+        else if (g.nslot == 8) launch_direct2_t<8, 0, O>(g, disk, n, ox, oy, oz, sweep, stats0, stats1, ovf, cz0, czs, st, tm);
+        else if (g.nslot == 16) launch_direct2_t<16, 0, O>(g, disk, n, ox, oy, oz, sweep, stats0, stats1, ovf, cz0, czs, st, tm);
+        else if (g.nslot == 32) launch_direct2_t<32, 0, O>(g, disk, n, ox, oy, oz, sweep, stats0, stats1, ovf, cz0, czs, st, tm);
+        else launch_direct2_t<64, 0, O>(g, disk, n, ox, oy, oz, sweep, stats0, stats1, ovf, cz0, czs, st, tm);
+    };
+    if (off32) go(std::true_type{});
+    else go(std::false_type{});
     return hipGetLastError();
 }
 
