@@ -1206,13 +1206,15 @@ int inject_delay(pmc_slab* s) {
 // bottom for p = 1) comes from the other side: one message each way, straight from and into the
 // state buffer (no packing).  The next run (parity 1-p) is the first to read H_p.  A single rank
 // without messages copies its own plane into its periodic halo.  On aux.
-int slab_exchange_run(pmc_ctx* c, int p, bool with_counts = false) {
+int slab_exchange_run(pmc_ctx* c, int p, bool with_counts = false, bool rows_written = false) {
     pmc_slab* s = c->slab;
     const int nz = c->P.nz_local;
     const size_t pf = plane_floats(c), pc = plane_cells(c);
     const int src = p == 0 ? 0 : nz - 1, dst = p == 0 ? nz : -1;
     if (!s->messages()) {
-        PMC_HIP(hipMemcpyAsync(disk_plane(c, dst), disk_plane(c, src), pf * 4, hipMemcpyDeviceToDevice, s->aux));
+        // (rows_written: the boundary launches already wrote the rows into the halo: direct halo)
+        if (!rows_written)
+            PMC_HIP(hipMemcpyAsync(disk_plane(c, dst), disk_plane(c, src), pf * 4, hipMemcpyDeviceToDevice, s->aux));
         if (with_counts)
             PMC_HIP(hipMemcpyAsync(n_plane(c, dst), n_plane(c, src), pc * 2, hipMemcpyDeviceToDevice, s->aux));
         return inject_delay(s);
@@ -1716,14 +1718,25 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
     // (the GPU tests compare every world size and chain count with the oracle's whole box).
     constexpr int kB = pmc_slab::kB;
     int k = 0;
+    // One rank without messages (the periodic single-rank slab, the strong-scaling rehearsal):
+    // PMC_SLAB_DIRECT_HALO=1 lets the boundary launches write each row they store into the halo
+    // plane that holds its periodic image as well (mirror mode 1), so the run's exchange copies
+    // nothing -- the one-GPU form of device-initiated halo writes
+    static const bool direct_halo_env = [] {
+        const char* v = std::getenv("PMC_SLAB_DIRECT_HALO");
+        return v && std::atoi(v) == 1;
+    }();
+    const bool direct_halo = direct_halo_env && !s->messages();
     auto phases = [&](hipStream_t st, int* ovf, int z0, int z1, int k0, int k1, bool boundary) -> int {
+        float* mir = nullptr;
+        if (boundary && direct_halo) mir = disk_plane(c, z0 == 0 ? nz : -1);   // plane 0 -> top halo, nz-1 -> bottom
         for (int kk = k0; kk < k1; ++kk) {
             int o[3];
             pmc_colour_offset(plan.order[kk], o);
             LaunchTiming lt;
             hipError_t le = boundary
                 ? launch_subsweep_boundary(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep, c->stats,
-                                           ovf, z0, z1, nullptr, 0, st, next_timing(c, 2, &lt))
+                                           ovf, z0, z1, mir, mir ? 1 : 0, st, next_timing(c, 2, &lt))
                 : launch_subsweep(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep, c->stats, ovf, z0,
                                   z1, st, next_timing(c, 0, &lt));   // every interior chain: kind 0
             if (le != hipSuccess) return hip_fail(le, "subsweep launch");
@@ -1779,7 +1792,7 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
             }();
             if (!skip_b && (r = phases(T, c->ovf_b, zb, zb + 1, k, k1, true))) return r;
             PMC_HIP(hipEventRecord(s->ev_run[kB][q], T));
-            if ((r = slab_exchange_run(c, q, merge_z))) return r;
+            if ((r = slab_exchange_run(c, q, merge_z, direct_halo))) return r;
             merge_z = false;
             s->pending_zdir = 0;
             return PMC_OK;
