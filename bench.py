@@ -3,6 +3,14 @@
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5|5box]
   torchrun --nproc-per-node N bench.py --gpus N ...     (one rank per GPU, z-slab decomposition)
 
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py launches the N rank processes
+itself (launch_ranks: fresh child processes with RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*, started
+before anything touches a GPU; the parent forwards their output, fails as soon as one rank fails
+and kills the rest), so `python bench.py --gpus 8` and the torchrun form run the same ranks.
+The ranks' control collectives (barriers, the max-over-ranks time, the gather of the box for the
+parity leg) run over gloo; the halo planes travel through the slab driver's transport (--transport:
+IPC pulls over xGMI by default, RCCL as the alternative).
+
 A "step" is one full MC sweep (8 checkerboard colour phases + shiftCells) with the state resident
 in HBM; w=rc=2.5, beta=0.3, sigma=0.5, n_M=10, nmax=16, Philox seed 1234, reference lattice start
 (kernel.cu:78-89).  The workloads are BASELINE.json's configs:
@@ -347,6 +355,76 @@ def rewarm(sim, one_sweep, finish, first: int, count: int, relink=None) -> None:
     sim.stats(reset=True)
     del save
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv: list, timeout_s: float) -> int:
+    """`bench.py --gpus N` without a launcher: start N rank processes of this script (RANK, LOCAL_RANK,
+    WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT in their environment) and wait for them.  The parent
+    touches no GPU (no torch, no libpmc: a process that initialised the GPU must never start or replace
+    programs); the ranks inherit stdout/stderr, so rank 0's JSON line is this command's output.  As soon
+    as one rank fails, or the time limit passes, the others are killed (their own process groups) and
+    the parent exits non-zero."""
+    import signal
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+
+    def kill_all():
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGTERM)
+                except OSError:
+                    pass
+        t_end = time.time() + 10
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, t_end - time.time()))
+            except subprocess.TimeoutExpired:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except OSError:
+                    pass
+                p.wait()
+
+    def on_signal(signum, _frame):
+        kill_all()
+        sys.exit(128 + signum)
+
+    signal.signal(signal.SIGTERM, on_signal)
+    signal.signal(signal.SIGINT, on_signal)
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      start_new_session=True))
+    print(f"bench.py: launched {n} rank processes (MASTER_PORT {port})", file=sys.stderr, flush=True)
+    t0 = time.time()
+    rc = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        if bad:
+            r, c = bad[0]
+            print(f"bench.py: rank {r} exited with {c}; stopping the other ranks", file=sys.stderr, flush=True)
+            rc = c if c > 0 else 128 - c
+            break
+        if all(c == 0 for c in codes):
+            break
+        if time.time() - t0 > timeout_s:
+            print(f"bench.py: ranks still running after {timeout_s:.0f} s; stopping them", file=sys.stderr, flush=True)
+            rc = 124
+            break
+        time.sleep(0.2)
+    kill_all()
+    return rc
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -383,19 +461,42 @@ def main() -> int:
     ap.add_argument("--halo", type=int, default=0, choices=(0, 1, 2),
                     help="slab halo planes per side: 2 = one exchange per sweep, the neighbour's boundary plane "
                          "visited redundantly (0: PMC_SLAB_HALO, default 1)")
+    ap.add_argument("--transport", choices=("auto", "ipc", "rccl", "local"), default=None,
+                    help="slab halo transport: ipc (peer buffers mapped over xGMI, pulled by the library's copy "
+                         "kernels), rccl, local (one rank: periodic halos by local copies), auto (ipc, else rccl on "
+                         "every rank).  Default: auto at N > 1, local for one-rank slabs (config 5: rccl)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="all ranks on GPU 0 (a multi-process correctness run on one GPU; needs the ipc transport)")
+    ap.add_argument("--rank-timeout", type=float, default=1500.0,
+                    help="--gpus N without a launcher: stop the ranks after this many seconds")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args.gpus, sys.argv[1:], args.rank_timeout)
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        print(f"bench.py rank {os.environ.get('RANK', '0')}/{os.environ['WORLD_SIZE']}: starting", file=sys.stderr,
+              flush=True)
     if args.xfer_delay_us > 0:
         os.environ["PMC_XFER_DELAY_US"] = str(args.xfer_delay_us)   # read by libpmc at its first exchange
 
+    import pmc_amd
     import torch
     import torch.distributed as dist
-    import pmc_amd
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}", file=sys.stderr)
+    if world > 1:
+        # fail before any GPU call when this rank has no device (pmc_device_count: PMC_ERR_NODEV)
+        try:
+            ndev = pmc_amd.device_count()
+        except pmc_amd.PmcError as e:
+            print(f"bench.py rank {rank}/{world}: {e}", file=sys.stderr, flush=True)
+            return 3
+        if not args.same_device and local >= ndev:
+            print(f"bench.py rank {rank}/{world}: LOCAL_RANK {local} but {ndev} GPU(s) visible", file=sys.stderr)
+            return 3
     config = args.config or ("4" if args.strong else ("3" if world == 1 else "4"))
     if args.emulate_ranks:
         if config != "4" or world != 1:
@@ -405,10 +506,11 @@ def main() -> int:
         config = "3"          # the 1-GPU point of the config-4 strong-scaling curve is config 3
     if config in ("2", "5box") and world > 1:
         raise SystemExit(f"--config {config} is a single-GPU configuration")
-    torch.cuda.set_device(local)
+    torch.cuda.set_device(0 if args.same_device else local)
     if world > 1:
+        # control collectives on the host (gloo); the halo data path is the slab driver's transport
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("gloo")
     stream = torch.cuda.Stream()
 
     def barrier():
@@ -461,8 +563,13 @@ def main() -> int:
     else:
         # the product multi-GPU path: sweep schedule + RCCL halo exchange in C (pmc_slab_*)
         from pmc_amd.slab import SlabDriver
-        use_rccl = world > 1 or args.self_rccl or (config == "5" and not args.local_halo)
-        drv = SlabDriver(cps=cps, nz_local=nz_local, rank=rank, world=world, stream=stream, use_rccl=use_rccl,
+        tp = args.transport
+        if tp is None:
+            tp = ("auto" if world > 1 else
+                  "rccl" if (args.self_rccl or (config == "5" and not args.local_halo)) else "local")
+        if args.same_device and tp not in ("ipc", "auto"):
+            raise SystemExit("--same-device needs the ipc transport (RCCL refuses two ranks on one GPU)")
+        drv = SlabDriver(cps=cps, nz_local=nz_local, rank=rank, world=world, stream=stream, transport=tp,
                          halo=args.halo)
         if config == "5" or args.emulate_ranks:
             drv.ctx.init_lattice_planes(atoms, cps)     # this rank's planes of the 256^3 / 8e7 (128^3 / 1e7) lattice
@@ -475,10 +582,12 @@ def main() -> int:
             drv.sweep(s)
 
         finish = drv.finish
+        tp_name = {"rccl": "RCCL", "ipc": "IPC pulls (pmc_slab_init_ipc: peer buffers mapped, copy kernels)",
+                   "local": "local copies"}[drv.transport]
         transport = (f"z-slab x{world}, {nz_local} planes per rank, "
                      + ("two halo planes per side (one exchange per sweep), " if drv.halo == 2 else "")
-                     + "halo planes over "
-                     + ("RCCL (C slab driver)" if use_rccl else "local copies (C slab driver)"))
+                     + f"halo planes over {tp_name} (C slab driver)"
+                     + (", all ranks on GPU 0" if args.same_device else ""))
 
     # warmup
     for s in range(args.warmup):
@@ -556,10 +665,10 @@ def main() -> int:
     tm = sim.timing_kinds(False)
     trials_local = st["trials"]
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        tr = torch.tensor([trials_local, st["accepted"]], dtype=torch.int64, device="cuda")
+        tr = torch.tensor([trials_local, st["accepted"]], dtype=torch.int64)
         dist.all_reduce(tr)
         trials_total, accepted_total = (int(v) for v in tr.tolist())
     else:
@@ -571,12 +680,12 @@ def main() -> int:
     e_end = sim.energy()
     de_timed = st["de_fixed"] / 2.0 ** 32
     if world > 1:   # slab energies count boundary pairs half on each side: the sum is the box's
-        ev = torch.tensor([e_start, e_end, de_timed], dtype=torch.float64, device="cuda")
+        ev = torch.tensor([e_start, e_end, de_timed], dtype=torch.float64)
         dist.all_reduce(ev)
         e_start, e_end, de_timed = (float(v) for v in ev.tolist())
     particles = int(n_owned.sum())
     if world > 1:
-        pt = torch.tensor([particles], dtype=torch.int64, device="cuda")
+        pt = torch.tensor([particles], dtype=torch.int64)
         dist.all_reduce(pt)
         particles = int(pt.item())
 
@@ -654,7 +763,7 @@ def main() -> int:
                     cpu = {"error": repr(e)}
             del whole
             barrier()
-            ok = torch.tensor([1 if (rank != 0 or ost is not None) else 0], device="cuda")
+            ok = torch.tensor([1 if (rank != 0 or ost is not None) else 0])
             if world > 1:
                 dist.broadcast(ok, src=0)
             if int(ok.item()):
@@ -666,7 +775,8 @@ def main() -> int:
         if args.emulate_ranks:
             name = (f"rehearsal of BASELINE config 4 at {args.emulate_ranks} ranks on 1 MI355X: one rank's slab "
                     f"({nz_local} planes of the 128^3 / 1e7 box, periodic, halos through "
-                    + ("RCCL" if use_rccl else "local copies") + "); value = ONE rank's rate")
+                    + {"rccl": "a one-rank RCCL communicator", "ipc": "the IPC transport's kernels (to itself)",
+                       "local": "local copies"}[drv.transport] + "); value = ONE rank's rate")
         out = {
             "metric": "MC trial-moves/s (whole node)",
             "value": value,

@@ -99,6 +99,9 @@ int pmc_state(pmc_ctx* ctx, float** disk, int16_t** n);
 int64_t pmc_storage_cells(const pmc_ctx* ctx);
 /* Last error message of this thread ("" if none). */
 const char* pmc_last_error(void);
+/* HIP devices visible to this process; PMC_ERR_NODEV (and *count = 0) when there is none.  Lets a
+ * launcher's rank process fail before it touches a device it does not have. */
+int pmc_device_count(int* count);
 
 /* ---- reference kernels ------------------------------------------------------------- */
 /* init_r (start.cu:47-58; index<N guard of kernel.cu:78-89): simple-cubic lattice of
@@ -202,6 +205,24 @@ int pmc_local_group_create(int world, pmc_local_group** out);
 void pmc_local_group_destroy(pmc_local_group* group);
 /* pmc_slab_init with the in-process transport: rank `rank` of group->world. */
 int pmc_slab_init_local(pmc_ctx* ctx, int rank, pmc_local_group* group);
+/* IPC transport: one PROCESS per rank on one node (one per GPU over xGMI, or several on one GPU),
+ * without RCCL.  Each rank exports its symmetric buffers -- the disk/n ping-pong pair, the
+ * two-plane-halo send planes, a flags buffer in uncached device memory -- with
+ * pmc_slab_ipc_handle; the caller gathers the world's blobs in rank order (any host collective,
+ * e.g. a gloo all_gather) and passes them to pmc_slab_init_ipc, which maps every peer's buffers
+ * (hipIpcOpenMemHandle).  An exchange is then three launches on the exchange stream and no host
+ * round trip: publish a sequence number and wait for the senders' (k_xfer_flag), pull every
+ * message straight from the sender's buffer (k_xfer_copy), wait until the readers have pulled.
+ * The messages, peers and matching are exactly RCCL's.  A wait that exceeds PMC_IPC_TIMEOUT_S
+ * (default 60 s) gives up and sets error flag bit 9 (512) instead of hanging the GPU.  The state
+ * buffers must not change afterwards (pmc_attach_state fails on an IPC slab).  The blob holding
+ * this context itself (a one-rank rehearsal: world = 1) maps nothing.  Replaces, like
+ * pmc_slab_init, the single-GPU loop start.cu:237-260. */
+#define PMC_IPC_HANDLE_BYTES 1024
+int pmc_slab_ipc_handle(pmc_ctx* ctx, unsigned char blob[PMC_IPC_HANDLE_BYTES]);
+/* blobs: world * PMC_IPC_HANDLE_BYTES bytes, rank r's blob at r * PMC_IPC_HANDLE_BYTES; collective
+ * in the sense that every rank must call it before the first exchange. */
+int pmc_slab_init_ipc(pmc_ctx* ctx, int rank, int world, const unsigned char* blobs);
 /* Refill both halo planes and their counts from the neighbours (after init_lattice, copy_in or
  * load_snapshot).  Collective. */
 int pmc_slab_exchange(pmc_ctx* ctx);
@@ -262,12 +283,14 @@ int pmc_run_small(pmc_ctx* ctx, uint32_t first_sweep, int count);
 
 /* ---- observables ------------------------------------------------------------------- */
 /* Total LJ energy of the owned cells' particles (calc_energy, kernel.cu:452-470, as an
- * O(N) cell-list sum; pairs across the slab boundary count half on each side). */
+ * O(N) cell-list sum; pairs across the slab boundary count half on each side).  A slab context
+ * must be flushed first after pmc_slab_sweep (pmc_slab_finish): a z shift's halo plane may still be
+ * pending, and that flush is collective, so pmc_energy refuses (PMC_ERR_ARG) instead of doing it. */
 int pmc_energy(pmc_ctx* ctx, double* e_out);
 /* Read and optionally reset the accumulated subsweep statistics (synchronises). */
 int pmc_stats_read(pmc_ctx* ctx, pmc_stats* out, int reset);
 /* Device error flags (bit 0: shift overflow, bit 1: assign overflow, bit 2: assign range, bits 3-4:
- * pmc_run_small);
+ * pmc_run_small; bit 9: an IPC-transport wait timed out);
  * synchronises; `reset` clears them. */
 int pmc_error_flags(pmc_ctx* ctx, uint32_t* flags, int reset);
 

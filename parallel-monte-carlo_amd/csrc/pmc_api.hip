@@ -12,6 +12,8 @@
 #include <mutex>
 #include <cstring>
 #include <string>
+#include <unistd.h>
+#include <utility>
 #include <vector>
 
 #include "pmc_internal.h"
@@ -40,6 +42,15 @@ struct pmc_ctx {
     int* ovf_aux2 = nullptr;               // fourth queue: the slab driver's third interior chain
     unsigned* run_ctl = nullptr;           // k_subsweep_run's claim heads and row counters (PMC_SLAB_RUNK)
     size_t ovf_bytes = 0;
+    // two-plane halos: the shifted send planes (planes 0, 1 then nz-2, nz-1, with their counts)
+    float* send_d = nullptr;
+    int16_t* send_n = nullptr;
+    // IPC halo transport (pmc_slab_ipc_handle / pmc_slab_init_ipc): sequence flags, reduction slots
+    // (uncached device memory other rank processes map), and the exchange count -- monotonic over
+    // the context's life, so a re-attached slab driver keeps agreeing with its peers' flags
+    uint64_t* xflags = nullptr;
+    int xflags_kind = 0;                   // 1 uncached, 2 fine-grained, 3 hipMalloc
+    uint64_t xseq = 0;
     int32_t* tmp_cnt = nullptr;
     int32_t* tmp_idx = nullptr;
     float* d_r = nullptr;
@@ -161,6 +172,8 @@ void drop_graph(pmc_ctx* c) {
 
 void drop_slab(pmc_ctx* c);
 int slab_join(pmc_ctx* c);   // slab driver streams -> context stream (defined with the driver)
+bool slab_is_ipc(const pmc_ctx* c);          // an IPC-transport slab driver is attached
+int slab_pending_zdir(const pmc_ctx* c);     // a deferred z-shift halo exchange is outstanding
 
 // the next timing slot when pmc_timing is on (nullptr otherwise): events ride on the launch's
 // dispatch packet (hipExtLaunchKernelGGL), no extra packets in the stream
@@ -289,6 +302,8 @@ void pmc_destroy(pmc_ctx* c) {
     if (c->ovf_b) (void)hipFree(c->ovf_b);
     if (c->ovf_aux2) (void)hipFree(c->ovf_aux2);
     if (c->run_ctl) (void)hipFree(c->run_ctl);
+    for (void* m : {(void*)c->send_d, (void*)c->send_n, (void*)c->xflags})
+        if (m) (void)hipFree(m);
     if (c->tmp_cnt) (void)hipFree(c->tmp_cnt);
     if (c->tmp_idx) (void)hipFree(c->tmp_idx);
     if (c->d_r) (void)hipFree(c->d_r);
@@ -315,8 +330,21 @@ int pmc_get_stream(pmc_ctx* c, void** stream) {
     return PMC_OK;
 }
 
+int pmc_device_count(int* count) {
+    if (!count) return fail(PMC_ERR_ARG, "null argument");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        (void)hipGetLastError();
+        *count = 0;
+        return fail(PMC_ERR_NODEV, "no HIP device");
+    }
+    *count = ndev;
+    return PMC_OK;
+}
+
 int pmc_attach_state(pmc_ctx* c, float* disk0, int16_t* n0, float* disk1, int16_t* n1) {
     if (!c || !disk0 || !n0 || !disk1 || !n1) return fail(PMC_ERR_ARG, "null argument");
+    if (slab_is_ipc(c)) return fail(PMC_ERR_ARG, "pmc_attach_state: the IPC transport's peers map the current buffers");
     PMC_HIP(hipStreamSynchronize(c->stream));
     drop_graph(c);
     free_state(c);
@@ -552,6 +580,10 @@ int pmc_run_graph(pmc_ctx* c, uint32_t first, int count) {
 // sum over the context's owned cells of the fixed-point pair terms (k_energy; the energy is half of
 // it, scaled by 2^-32): exact, and exactly additive over slabs
 int energy_fixed(pmc_ctx* c, int64_t* fixed) {
+    // the energy reads both halos: a z shift's deferred halo exchange must be flushed first, and the
+    // flush is collective (pmc_slab_finish / pmc_slab_observables do it on every rank)
+    if (slab_pending_zdir(c))
+        return fail(PMC_ERR_ARG, "pmc_energy: a slab halo exchange is pending (call pmc_slab_finish first)");
     if (int rj = slab_join(c)) return rj;
     PMC_HIP(hipMemsetAsync(c->eacc, 0, sizeof(unsigned long long) * kStatSlots, c->stream));
     if (!c->segq) PMC_HIP(hipMalloc(&c->segq, sizeof(int) * (1 + energy_segments(c->G))));
@@ -927,12 +959,21 @@ int nccl_fail(ncclResult_t e, const char* what) {
 //   * an in-process group (pmc_local_group): W slab contexts of ONE process, one host thread per
 //     rank, device-to-device copies ordered by HIP events and a host barrier -- the same schedule,
 //     peers and message lists as RCCL, so W ranks run on one GPU ("a local-copy halo
-//     transport behind the same interface as the RCCL transport").
+//     transport behind the same interface as the RCCL transport");
+//   * IPC (pmc_slab_init_ipc): one process per rank on one node -- one per GPU, or several on one
+//     GPU -- each mapping its peers' state buffers and flags (hipIpcOpenMemHandle over xGMI); the
+//     receiver pulls every message straight from the sender's buffer with its own copy kernel,
+//     ordered by per-rank sequence flags in device memory (pmc_kernels.hip, k_xfer_*): no host
+//     round trip, no proxy thread, no RCCL channel set-up per message.
 // A single rank without either keeps its periodic halos by local copies (no messages at all).
 struct XferMsg {
     void* buf;
     size_t bytes;
     int peer;
+    // receives: where the sender's source lies, named by the SAME buffer and offset in this rank's
+    // own memory -- every rank has the identical layout and ping-pong index (symmetric buffers), so
+    // the IPC transport maps it to the peer's copy (pmc_slab_init_ipc)
+    const void* sym = nullptr;
 };
 
 struct pmc_local_group {
@@ -985,6 +1026,12 @@ void group_break(pmc_local_group* g) {
 
 }  // namespace
 
+// IPC transport: the symmetric buffers a peer maps, and the layout of the flags buffer (u64 slots;
+// each flag on its own 128-B line)
+constexpr int kIpcBufs = 7;               // disk[0], disk[1], n[0], n[1], send_d, send_n, xflags
+constexpr int kFlagReady = 0, kFlagPulled = 16, kFlagDone = 32, kFlagRed = 48, kFlagGather = 64;
+constexpr size_t kFlagBytes = sizeof(uint64_t) * (kFlagGather + 8 * kXferMax);
+
 struct pmc_slab {
     int rank = 0, world = 1, below = 0, above = 0;
     ncclComm_t comm = nullptr;            // RCCL transport
@@ -1015,10 +1062,22 @@ struct pmc_slab {
     // the exchange of sweep `pending_sweep`'s first run carries it (same messages plus the counts)
     int pending_zdir = 0;
     uint32_t pending_sweep = 0;
-    bool messages() const { return comm != nullptr || group != nullptr; }
+    // IPC transport: every peer's symmetric buffers (disk0, disk1, n0, n1, send_d, send_n, flags)
+    // mapped into this process (this rank's own pointers for itself)
+    bool ipc = false;
+    struct IpcPeer {
+        void* base[kIpcBufs] = {};
+        std::vector<void*> opened;        // hipIpcOpenMemHandle mappings to close
+    };
+    std::vector<IpcPeer> peers;
+    uint64_t ipc_timeout = 0;             // wait limit, ticks of the 100 MHz real-time counter
+    bool messages() const { return comm != nullptr || group != nullptr || ipc; }
 };
 
 namespace {
+
+bool slab_is_ipc(const pmc_ctx* c) { return c->slab && c->slab->ipc; }
+int slab_pending_zdir(const pmc_ctx* c) { return c->slab ? c->slab->pending_zdir : 0; }
 
 void drop_slab(pmc_ctx* c) {
     pmc_slab* s = c->slab;
@@ -1036,8 +1095,9 @@ void drop_slab(pmc_ctx* c) {
         (void)hipStreamSynchronize(s->hr);
         (void)hipStreamDestroy(s->hr);
     }
-    for (void* m : {(void*)s->send_d, (void*)s->send_n, (void*)s->stats_scratch})
-        if (m) (void)hipFree(m);
+    if (s->stats_scratch) (void)hipFree(s->stats_scratch);   // (the send planes are the context's)
+    for (pmc_slab::IpcPeer& pr : s->peers)
+        for (void* m : pr.opened) (void)hipIpcCloseMemHandle(m);
     for (hipEvent_t e : {s->ev_i, s->ev_b, s->ev_t, s->ev_x, s->ev_hp})
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t* e : s->run_events())
@@ -1096,13 +1156,81 @@ int slab_join(pmc_ctx* c) {
 void xfer_send(pmc_slab* s, const void* buf, size_t bytes, int peer) {
     s->sends.push_back({const_cast<void*>(buf), bytes, peer});
 }
-void xfer_recv(pmc_slab* s, void* buf, size_t bytes, int peer) { s->recvs.push_back({buf, bytes, peer}); }
+void xfer_recv(pmc_slab* s, void* buf, size_t bytes, int peer, const void* sym) {
+    s->recvs.push_back({buf, bytes, peer, sym});
+}
 
-// carry the queued messages on the aux stream (RCCL group, or the in-process group's copies)
-int xfer_run(pmc_slab* s) {
+// this rank's symmetric buffers, in the order of pmc_slab::IpcPeer::base
+void ipc_local_bufs(const pmc_ctx* c, const void* base[kIpcBufs], size_t bytes[kIpcBufs]) {
+    const size_t db = sizeof(float) * 3 * (size_t)c->P.nmax * (size_t)c->cells, nb = sizeof(int16_t) * (size_t)c->cells;
+    const size_t pf = (size_t)c->P.cps_x * c->P.cps_y * 3 * c->P.nmax, pc = (size_t)c->P.cps_x * c->P.cps_y;
+    const void* b[kIpcBufs] = {c->disk[0], c->disk[1], c->n[0], c->n[1], c->send_d, c->send_n, c->xflags};
+    const size_t z[kIpcBufs] = {db, db, nb, nb, c->send_d ? 4 * pf * sizeof(float) : 0,
+                                c->send_n ? 4 * pc * sizeof(int16_t) : 0, c->xflags ? kFlagBytes : 0};
+    for (int i = 0; i < kIpcBufs; ++i) {
+        base[i] = b[i];
+        bytes[i] = b[i] ? z[i] : 0;
+    }
+}
+
+// the peer's copy of this rank's symmetric address `sym` (nullptr if `sym` lies in none of them)
+const void* ipc_translate(const pmc_ctx* c, const pmc_slab* s, int peer, const void* sym, size_t bytes) {
+    const void* base[kIpcBufs];
+    size_t size[kIpcBufs];
+    ipc_local_bufs(c, base, size);
+    const uintptr_t a = (uintptr_t)sym;
+    for (int i = 0; i < kIpcBufs; ++i) {
+        const uintptr_t b = (uintptr_t)base[i];
+        if (b && a >= b && a + bytes <= b + size[i] && s->peers[(size_t)peer].base[i])
+            return (const char*)s->peers[(size_t)peer].base[i] + (a - b);
+    }
+    return nullptr;
+}
+
+int xfer_seg(XferCopy& cp, const void* src, void* dst, size_t bytes) {
+    if (cp.n >= kXferMax) return fail(PMC_ERR_ARG, "IPC transport: too many messages in one exchange");
+    int sh = 4;
+    while (sh > 0 && ((((uintptr_t)src | (uintptr_t)dst | (uintptr_t)bytes) & ((1u << sh) - 1)) != 0)) --sh;
+    cp.seg[cp.n++] = {src, dst, (uint64_t)bytes, sh};
+    return PMC_OK;
+}
+
+void xfer_flag_add(XferFlags& w, const uint64_t* f) {
+    for (int i = 0; i < w.n; ++i)
+        if (w.flag[i] == f) return;
+    w.flag[w.n++] = f;
+}
+
+// exchange k over IPC: ready[me] = k and wait for the senders' ready; pull every message from the
+// peer's buffer (the copy kernel's last block stores pulled[me] = k); wait for the readers' pulled
+// before the exchange stream may overwrite this rank's buffers again.  Three launches on aux.
+int ipc_run(pmc_ctx* c, const std::vector<XferMsg>& sends, const std::vector<XferMsg>& recvs) {
+    pmc_slab* s = c->slab;
+    const uint64_t seq = ++c->xseq;
+    XferFlags wr{}, wp{};
+    XferCopy cp{};
+    auto pflags = [&](int p) { return reinterpret_cast<const uint64_t*>(s->peers[(size_t)p].base[kIpcBufs - 1]); };
+    for (const XferMsg& m : recvs) {
+        const void* src = m.sym ? ipc_translate(c, s, m.peer, m.sym, m.bytes) : nullptr;
+        if (!src) return fail(PMC_ERR_ARG, "IPC transport: a receive's source is not in a symmetric buffer");
+        if (int rc = xfer_seg(cp, src, m.buf, m.bytes)) return rc;
+        xfer_flag_add(wr, pflags(m.peer) + kFlagReady);
+    }
+    for (const XferMsg& m : sends) xfer_flag_add(wp, pflags(m.peer) + kFlagPulled);
+    hipError_t e = launch_xfer_flag(c->xflags + kFlagReady, seq, wr, s->ipc_timeout, c->flags, s->aux);
+    if (e == hipSuccess)
+        e = launch_xfer_copy(cp, c->xflags + kFlagPulled, seq, reinterpret_cast<unsigned*>(c->xflags + kFlagDone), s->aux);
+    if (e == hipSuccess) e = launch_xfer_flag(nullptr, seq, wp, s->ipc_timeout, c->flags, s->aux);
+    return e == hipSuccess ? PMC_OK : hip_fail(e, "IPC halo exchange");
+}
+
+// carry the queued messages on the aux stream (RCCL group, IPC pulls, or the in-process group's copies)
+int xfer_run(pmc_ctx* c) {
+    pmc_slab* s = c->slab;
     std::vector<XferMsg> sends, recvs;
     sends.swap(s->sends);
     recvs.swap(s->recvs);
+    if (s->ipc) return ipc_run(c, sends, recvs);
     if (s->comm) {
         Rccl& R = rccl();
         PMC_NCCL(R.group_start());
@@ -1174,6 +1302,15 @@ int xfer_run(pmc_slab* s) {
 
 size_t plane_floats(const pmc_ctx* c) { return (size_t)c->P.cps_x * c->P.cps_y * 3 * c->P.nmax; }
 size_t plane_cells(const pmc_ctx* c) { return (size_t)c->P.cps_x * c->P.cps_y; }
+
+// the two-plane-halo send buffer (4 planes and their counts), context-owned: the IPC transport
+// exports it before the slab driver attaches
+hipError_t ensure_send_planes(pmc_ctx* c) {
+    hipError_t e = hipSuccess;
+    if (!c->send_d) e = hipMalloc(&c->send_d, 4 * plane_floats(c) * sizeof(float));
+    if (e == hipSuccess && !c->send_n) e = hipMalloc(&c->send_n, 4 * plane_cells(c) * sizeof(int16_t));
+    return e;
+}
 // storage plane of local plane z (-halo .. -1 bottom halos, nz_local .. nz_local-1+halo top halos)
 float* disk_plane(pmc_ctx* c, int z) { return c->disk[c->cur] + (size_t)(z + c->P.halo) * plane_floats(c); }
 int16_t* n_plane(pmc_ctx* c, int z) { return c->n[c->cur] + (size_t)(z + c->P.halo) * plane_cells(c); }
@@ -1222,9 +1359,9 @@ int slab_exchange_run(pmc_ctx* c, int p, bool with_counts = false, bool rows_wri
     const int to = p == 0 ? s->below : s->above, from = p == 0 ? s->above : s->below;
     xfer_send(s, disk_plane(c, src), pf * 4, to);
     if (with_counts) xfer_send(s, n_plane(c, src), pc * 2, to);
-    xfer_recv(s, disk_plane(c, dst), pf * 4, from);
-    if (with_counts) xfer_recv(s, n_plane(c, dst), pc * 2, from);
-    if (int rc = xfer_run(s)) return rc;
+    xfer_recv(s, disk_plane(c, dst), pf * 4, from, disk_plane(c, src));
+    if (with_counts) xfer_recv(s, n_plane(c, dst), pc * 2, from, n_plane(c, src));
+    if (int rc = xfer_run(c)) return rc;
     return inject_delay(s);
 }
 
@@ -1255,11 +1392,11 @@ int slab_exchange_full(pmc_ctx* c, bool from_send = false) {
     xfer_send(s, lo_n, nb, s->below);
     xfer_send(s, hi_d, db, s->above);
     xfer_send(s, hi_n, nb, s->above);
-    xfer_recv(s, disk_plane(c, nz), db, s->above);
-    xfer_recv(s, n_plane(c, nz), nb, s->above);
-    xfer_recv(s, disk_plane(c, -h), db, s->below);
-    xfer_recv(s, n_plane(c, -h), nb, s->below);
-    return xfer_run(s);
+    xfer_recv(s, disk_plane(c, nz), db, s->above, lo_d);
+    xfer_recv(s, n_plane(c, nz), nb, s->above, lo_n);
+    xfer_recv(s, disk_plane(c, -h), db, s->below, hi_d);
+    xfer_recv(s, n_plane(c, -h), nb, s->below, hi_n);
+    return xfer_run(c);
 }
 
 // after a shift along z in direction dir: the halo on the +dir side takes the neighbour's new
@@ -1277,9 +1414,9 @@ int slab_exchange_zplane(pmc_ctx* c, int dir) {
     const int to = dir > 0 ? s->below : s->above, from = dir > 0 ? s->above : s->below;
     xfer_send(s, disk_plane(c, src), pf * 4, to);
     xfer_send(s, n_plane(c, src), pc * 2, to);
-    xfer_recv(s, disk_plane(c, dst), pf * 4, from);
-    xfer_recv(s, n_plane(c, dst), pc * 2, from);
-    if (int rc = xfer_run(s)) return rc;
+    xfer_recv(s, disk_plane(c, dst), pf * 4, from, disk_plane(c, src));
+    xfer_recv(s, n_plane(c, dst), pc * 2, from, n_plane(c, src));
+    if (int rc = xfer_run(c)) return rc;
     return inject_delay(s);
 }
 
@@ -1365,14 +1502,14 @@ int slab_attach(pmc_ctx* c, int rank, int world, bool messages) {
             return hip_fail(e, "hipStreamCreate");
         }
         const size_t sb = sizeof(unsigned long long) * kStatCounters * kStatSlots;
-        if ((e = hipMalloc(&s->send_d, 4 * plane_floats(c) * sizeof(float))) != hipSuccess ||
-            (e = hipMalloc(&s->send_n, 4 * plane_cells(c) * sizeof(int16_t))) != hipSuccess ||
-            (e = hipMalloc(&s->stats_scratch, sb)) != hipSuccess ||
+        if ((e = ensure_send_planes(c)) != hipSuccess || (e = hipMalloc(&s->stats_scratch, sb)) != hipSuccess ||
             (e = hipMemsetAsync(s->stats_scratch, 0, sb, c->stream)) != hipSuccess) {
             drop_slab(c);
             return hip_fail(e, "hipMalloc (two-plane halos)");
         }
     }
+    s->send_d = c->send_d;
+    s->send_n = c->send_n;
     for (int j = 0; j + 1 < s->chains; ++j)
         if ((e = hipStreamCreateWithFlags(&s->hi[j], hipStreamNonBlocking)) != hipSuccess) {
             drop_slab(c);
@@ -1465,6 +1602,156 @@ int pmc_slab_init_local(pmc_ctx* c, int rank, pmc_local_group* g) {
     std::lock_guard<std::mutex> lk(g->m);
     g->slot[rank].joined = true;
     c->slab->group = g;
+    return PMC_OK;
+}
+
+// ---- IPC transport ---------------------------------------------------------------------------
+namespace {
+
+constexpr uint32_t kIpcMagic = 0x49434d50u;   // "PMCI"
+constexpr uint32_t kIpcVersion = 1;
+struct IpcBlob {
+    uint32_t magic, version;
+    uint64_t token;                     // (pid << 32) ^ context address: the exporting process + context
+    int32_t pid, device;
+    int32_t cps_x, cps_y, nz_local, halo, nmax, world_hint;
+    struct Buf {
+        hipIpcMemHandle_t handle;
+        uint64_t offset, bytes;         // the buffer inside the exported allocation
+    } buf[kIpcBufs];
+};
+static_assert(sizeof(IpcBlob) <= PMC_IPC_HANDLE_BYTES, "IPC blob size");
+
+uint64_t ipc_token(const pmc_ctx* c) { return ((uint64_t)(uint32_t)getpid() << 32) ^ (uint64_t)(uintptr_t)c; }
+
+// the flags buffer: uncached device memory (every flag access goes to memory: other processes and
+// other GPUs see it without cache maintenance), else fine-grained, else plain -- the first kind
+// whose IPC export works
+int ensure_xflags(pmc_ctx* c) {
+    if (c->xflags) return PMC_OK;
+    const unsigned kinds[2] = {hipDeviceMallocUncached, hipDeviceMallocFinegrained};
+    for (int k = 0; k < 3 && !c->xflags; ++k) {
+        void* p = nullptr;
+        hipError_t e = k < 2 ? hipExtMallocWithFlags(&p, kFlagBytes, kinds[k]) : hipMalloc(&p, kFlagBytes);
+        if (e != hipSuccess) continue;
+        hipIpcMemHandle_t h;
+        if (hipIpcGetMemHandle(&h, p) != hipSuccess) {
+            (void)hipGetLastError();
+            (void)hipFree(p);
+            continue;
+        }
+        c->xflags = (uint64_t*)p;
+        c->xflags_kind = k + 1;
+    }
+    if (!c->xflags) return fail(PMC_ERR_HIP, "IPC transport: no exportable device memory for the flags");
+    PMC_HIP(hipMemsetAsync(c->xflags, 0, kFlagBytes, c->stream));
+    PMC_HIP(hipStreamSynchronize(c->stream));
+    return PMC_OK;
+}
+
+}  // namespace
+
+int pmc_slab_ipc_handle(pmc_ctx* c, unsigned char* blob) {
+    if (!c || !blob) return fail(PMC_ERR_ARG, "null argument");
+    if (c->P.halo < 1) return fail(PMC_ERR_ARG, "pmc_slab_ipc_handle needs a slab context (halo = 1 or 2)");
+    if (int rc = ensure_xflags(c)) return rc;
+    if (c->P.halo == 2) PMC_HIP(ensure_send_planes(c));
+    IpcBlob b;
+    std::memset(&b, 0, sizeof b);
+    b.magic = kIpcMagic;
+    b.version = kIpcVersion;
+    b.token = ipc_token(c);
+    b.pid = (int32_t)getpid();
+    PMC_HIP(hipGetDevice(&b.device));
+    b.cps_x = c->P.cps_x;
+    b.cps_y = c->P.cps_y;
+    b.nz_local = c->P.nz_local;
+    b.halo = c->P.halo;
+    b.nmax = c->P.nmax;
+    const void* base[kIpcBufs];
+    size_t bytes[kIpcBufs];
+    ipc_local_bufs(c, base, bytes);
+    for (int i = 0; i < kIpcBufs; ++i) {
+        if (!base[i]) continue;
+        void* alloc = nullptr;
+        size_t asize = 0;
+        PMC_HIP(hipMemGetAddressRange(&alloc, &asize, const_cast<void*>(base[i])));
+        PMC_HIP(hipIpcGetMemHandle(&b.buf[i].handle, alloc));
+        b.buf[i].offset = (uint64_t)((uintptr_t)base[i] - (uintptr_t)alloc);
+        b.buf[i].bytes = bytes[i];
+    }
+    std::memset(blob, 0, PMC_IPC_HANDLE_BYTES);
+    std::memcpy(blob, &b, sizeof b);
+    return PMC_OK;
+}
+
+int pmc_slab_init_ipc(pmc_ctx* c, int rank, int world, const unsigned char* blobs) {
+    if (!c || !blobs || world < 1 || rank < 0 || rank >= world) return fail(PMC_ERR_ARG, "bad argument");
+    if (world > kXferMax) return fail(PMC_ERR_ARG, "IPC transport: at most 16 ranks");
+    std::vector<IpcBlob> bl((size_t)world);
+    for (int p = 0; p < world; ++p) {
+        std::memcpy(&bl[(size_t)p], blobs + (size_t)p * PMC_IPC_HANDLE_BYTES, sizeof(IpcBlob));
+        const IpcBlob& b = bl[(size_t)p];
+        if (b.magic != kIpcMagic || b.version != kIpcVersion)
+            return fail(PMC_ERR_ARG, "IPC transport: not a pmc_slab_ipc_handle blob");
+        if (b.cps_x != c->P.cps_x || b.cps_y != c->P.cps_y || b.nz_local != c->P.nz_local || b.halo != c->P.halo ||
+            b.nmax != c->P.nmax)
+            return fail(PMC_ERR_ARG, "IPC transport: the ranks' slab geometries differ");
+    }
+    if (!c->xflags || bl[(size_t)rank].token != ipc_token(c))
+        return fail(PMC_ERR_ARG, "IPC transport: blob[rank] is not this context's pmc_slab_ipc_handle");
+    int rc = slab_attach(c, rank, world, true);
+    if (rc) return rc;
+    pmc_slab* s = c->slab;
+    s->peers.assign((size_t)world, pmc_slab::IpcPeer{});
+    const void* mine[kIpcBufs];
+    size_t mine_bytes[kIpcBufs];
+    ipc_local_bufs(c, mine, mine_bytes);
+    for (int p = 0; p < world; ++p) {
+        const IpcBlob& b = bl[(size_t)p];
+        pmc_slab::IpcPeer& pr = s->peers[(size_t)p];
+        if (b.token == ipc_token(c)) {            // this context itself (a one-rank IPC rehearsal)
+            for (int i = 0; i < kIpcBufs; ++i) pr.base[i] = const_cast<void*>(mine[i]);
+            continue;
+        }
+        if (b.pid == (int32_t)getpid()) {
+            drop_slab(c);
+            return fail(PMC_ERR_ARG, "IPC transport: two ranks in one process (use pmc_slab_init_local)");
+        }
+        std::vector<std::pair<std::string, void*>> seen;   // one mapping per exported allocation
+        for (int i = 0; i < kIpcBufs; ++i) {
+            if (!b.buf[i].bytes) continue;
+            if (b.buf[i].bytes != mine_bytes[i]) {
+                drop_slab(c);
+                return fail(PMC_ERR_ARG, "IPC transport: a peer's buffer sizes differ");
+            }
+            const std::string key(reinterpret_cast<const char*>(&b.buf[i].handle), sizeof(hipIpcMemHandle_t));
+            void* m = nullptr;
+            for (auto& kv : seen)
+                if (kv.first == key) m = kv.second;
+            if (!m) {
+                hipError_t e = hipIpcOpenMemHandle(&m, b.buf[i].handle, hipIpcMemLazyEnablePeerAccess);
+                if (e != hipSuccess) {
+                    drop_slab(c);
+                    return hip_fail(e, "hipIpcOpenMemHandle (IPC transport)");
+                }
+                pr.opened.push_back(m);
+                seen.emplace_back(key, m);
+            }
+            pr.base[i] = (char*)m + b.buf[i].offset;
+        }
+        if (!pr.base[kIpcBufs - 1]) {
+            drop_slab(c);
+            return fail(PMC_ERR_ARG, "IPC transport: a peer exported no flags");
+        }
+    }
+    static const double timeout_s = [] {
+        const char* v = std::getenv("PMC_IPC_TIMEOUT_S");
+        const double t = v ? std::atof(v) : 0.0;
+        return t > 0.0 ? t : 60.0;
+    }();
+    s->ipc_timeout = (uint64_t)(timeout_s * 1e8);
+    s->ipc = true;
     return PMC_OK;
 }
 
@@ -1953,6 +2240,36 @@ int pmc_slab_observables(pmc_ctx* c, int with_energy, pmc_stats* out, double* e_
         if (e == hipSuccess) e = hipStreamSynchronize(s->aux);
         (void)hipFree(d);
         if (e != hipSuccess) return hip_fail(e, "observables all-reduce");
+    } else if (s->ipc) {
+        // every rank's five sums into its flags buffer; each rank pulls all of them (one exchange:
+        // ready, pull, pulled -- the sequence numbers of the halo exchanges continue)
+        const uint64_t seq = ++c->xseq;
+        XferFlags wr{}, wp{};
+        XferCopy cp{};
+        for (int p = 0; p < s->world; ++p) {
+            const uint64_t* pf = reinterpret_cast<const uint64_t*>(s->peers[(size_t)p].base[kIpcBufs - 1]);
+            if (int rc = xfer_seg(cp, pf + kFlagRed, c->xflags + kFlagGather + 8 * p, sizeof v)) return rc;
+            if (p != s->rank) {
+                xfer_flag_add(wr, pf + kFlagReady);
+                xfer_flag_add(wp, pf + kFlagPulled);
+            }
+        }
+        PMC_HIP(hipMemcpyAsync(c->xflags + kFlagRed, v, sizeof v, hipMemcpyHostToDevice, s->aux));
+        PMC_HIP(launch_xfer_flag(c->xflags + kFlagReady, seq, wr, s->ipc_timeout, c->flags, s->aux));
+        PMC_HIP(launch_xfer_copy(cp, c->xflags + kFlagPulled, seq, reinterpret_cast<unsigned*>(c->xflags + kFlagDone),
+                                 s->aux));
+        PMC_HIP(launch_xfer_flag(nullptr, seq, wp, s->ipc_timeout, c->flags, s->aux));
+        std::vector<uint64_t> h((size_t)8 * s->world);
+        PMC_HIP(hipMemcpyAsync(h.data(), c->xflags + kFlagGather, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                               s->aux));
+        PMC_HIP(hipStreamSynchronize(s->aux));
+        uint32_t fl = 0;
+        PMC_HIP(hipMemcpy(&fl, c->flags, 4, hipMemcpyDeviceToHost));
+        if (fl & 512u) return fail(PMC_ERR_HIP, "IPC transport: a peer did not arrive (wait timed out, error flag 512)");
+        for (int k = 0; k < 5; ++k) {
+            v[k] = 0;
+            for (int p = 0; p < s->world; ++p) v[k] += h[(size_t)8 * p + k];
+        }
     } else if (s->group) {
         pmc_local_group* g = s->group;
         {

@@ -145,6 +145,27 @@ hipError_t launch_energy(const DevGeom& g, const float* disk, const int16_t* n,
 hipError_t launch_colour_rows(const DevGeom& g, const float* src, float* dst, int colour, int mode, hipStream_t st);
 // rehearsal only: a one-wave kernel that occupies `st` for `us` microseconds (injected exchange delay)
 hipError_t launch_spin(double us, hipStream_t st);
+// IPC halo transport (pmc_kernels.hip, pmc_slab_init_ipc): sequence flags and the pull copy
+constexpr int kXferMax = 16;       // flags waited on / segments copied per launch (peers <= 16)
+struct XferFlags {
+    const uint64_t* flag[kXferMax];
+    int n;
+};
+struct XferSeg {
+    const void* src;
+    void* dst;
+    uint64_t bytes;
+    int shift;                     // log2 of the copy unit (1..16 B): divides src, dst and bytes
+};
+struct XferCopy {
+    XferSeg seg[kXferMax];
+    int n;
+};
+// mine (may be null) := seq, then wait until every w.flag[i] >= seq (timeout: error flag 512)
+hipError_t launch_xfer_flag(uint64_t* mine, uint64_t seq, const XferFlags& w, uint64_t timeout_ticks, uint32_t* err,
+                            hipStream_t st);
+// copy every segment; the last block stores *pulled = seq (pulled may be null: no signal)
+hipError_t launch_xfer_copy(const XferCopy& cp, uint64_t* pulled, uint64_t seq, unsigned* done, hipStream_t st);
 hipError_t launch_selftest(const uint32_t* words, int count, float* out_f, double* out_d,
                            float rc2, hipStream_t st);
 

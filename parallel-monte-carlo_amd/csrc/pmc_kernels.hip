@@ -2517,6 +2517,114 @@ hipError_t launch_spin(double us, hipStream_t st) {
 }
 
 // ------------------------------------------------------------------------------------------
+// IPC halo transport (pmc_slab_init_ipc): the slab driver's point-to-point messages between rank
+// processes of one node (or several processes on one GPU), through IPC-mapped peer buffers and
+// per-rank sequence flags in uncached device memory -- no host round trip per exchange.  Exchange k
+// on the exchange stream is three launches:
+//   k_xfer_flag (signal + wait): ready[me] = k, then wait until ready[p] >= k for every peer p this
+//     rank receives from (their send planes are complete: stream order on their side);
+//   k_xfer_copy: pull every message from the peer's buffer into ours, grid-wide; the last block
+//     to finish stores pulled[me] = k (every read of the peers' buffers is done);
+//   k_xfer_flag (wait only): until pulled[p] >= k for every peer p that reads our buffers, so the
+//     exchange stream's later work may overwrite them.
+// The copy is a separate launch from the wait on purpose: it starts after the wait kernel has
+// completed, so the kernel-start acquire the command processor performs orders its reads after
+// the peers' kernel-end releases, exactly as a cross-stream event wait would (no in-kernel cache
+// maintenance on peer data).  Waits give up after `timeout` ticks of the 100 MHz real-time
+// counter and set error-flag bit 9 (value 512) instead of hanging the GPU.
+// ------------------------------------------------------------------------------------------
+namespace {
+
+__device__ __forceinline__ uint64_t flag_load(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ void flag_store(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void __launch_bounds__(kWave) k_xfer_flag(uint64_t* mine, uint64_t seq, XferFlags w, uint64_t timeout,
+                                                      uint32_t* err) {
+    if (threadIdx.x != 0) return;
+    if (mine) flag_store(mine, seq);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (int i = 0; i < w.n; ++i) {
+        while (flag_load(w.flag[i]) < seq) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
+                atomicOr(err, 512u);
+                return;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+}
+
+template <class U>
+__device__ __forceinline__ void xfer_units(const XferSeg& s, int shift) {
+    const U* __restrict__ src = reinterpret_cast<const U*>(s.src);
+    U* __restrict__ dst = reinterpret_cast<U*>(s.dst);
+    const uint64_t n = s.bytes >> shift;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // four independent loads in flight per lane before their stores
+    for (; i + 3 * stride < n; i += 4 * stride) {
+        const U a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+        dst[i] = a;
+        dst[i + stride] = b;
+        dst[i + 2 * stride] = c;
+        dst[i + 3 * stride] = d;
+    }
+    for (; i < n; i += stride) dst[i] = src[i];
+}
+
+__global__ void __launch_bounds__(256) k_xfer_copy(XferCopy cp, uint64_t* pulled, uint64_t seq, unsigned* done) {
+    for (int k = 0; k < cp.n; ++k) {
+        const XferSeg& s = cp.seg[k];
+        switch (s.shift) {
+            case 4: xfer_units<uint4>(s, 4); break;
+            case 3: xfer_units<uint2>(s, 3); break;
+            case 2: xfer_units<uint32_t>(s, 2); break;
+            case 1: xfer_units<uint16_t>(s, 1); break;
+            default: xfer_units<uint8_t>(s, 0); break;
+        }
+    }
+    if (!pulled) return;
+    __syncthreads();                      // every load of this block has returned (its stores used them)
+    if (threadIdx.x == 0) {
+        const unsigned prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (prev == gridDim.x - 1) {
+            __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            flag_store(pulled, seq);
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t launch_xfer_flag(uint64_t* mine, uint64_t seq, const XferFlags& w, uint64_t timeout_ticks, uint32_t* err,
+                            hipStream_t st) {
+    if (w.n < 0 || w.n > kXferMax) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_xfer_flag, dim3(1), dim3(kWave), 0, st, mine, seq, w, timeout_ticks, err);
+    return hipGetLastError();
+}
+
+hipError_t launch_xfer_copy(const XferCopy& cp, uint64_t* pulled, uint64_t seq, unsigned* done, hipStream_t st) {
+    if (cp.n < 0 || cp.n > kXferMax) return hipErrorInvalidValue;
+    uint64_t units = 0;   // 16-B units of the largest segment set the grid: ~4 per lane
+    for (int k = 0; k < cp.n; ++k) {
+        const XferSeg& s = cp.seg[k];
+        if (s.shift < 0 || s.shift > 4 || (s.bytes & ((1ull << s.shift) - 1)) ||
+            (((uintptr_t)s.src | (uintptr_t)s.dst) & ((1ull << s.shift) - 1)))
+            return hipErrorInvalidValue;
+        units += (s.bytes + 15) / 16;
+    }
+    const uint64_t want = (units + 1023) / 1024;
+    const unsigned blocks = (unsigned)(want < 1 ? 1 : want > 512 ? 512 : want);
+    hipLaunchKernelGGL(k_xfer_copy, dim3(blocks), dim3(256), 0, st, cp, pulled, seq, done);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------
 // hipLaunchKernelGGL, or with dispatch-packet timing events when tm is given

@@ -47,6 +47,7 @@ class Result(C.Structure):
 
 PMC_FLAG_FULL_SHUFFLE = 1
 PMC_OK, PMC_ERR_ARG, PMC_ERR_HIP, PMC_ERR_OVERFLOW, PMC_ERR_RANGE, PMC_ERR_NODEV = 0, -1, -2, -3, -4, -5
+PMC_IPC_HANDLE_BYTES = 1024     # include/pmc.h
 
 
 class PmcError(RuntimeError):
@@ -115,6 +116,9 @@ def lib():
         _sig(L, "pmc_local_group_create", i32, i32, C.POINTER(_vp))
         _sig(L, "pmc_local_group_destroy", None, _vp)
         _sig(L, "pmc_slab_init_local", i32, _vp, i32, _vp)
+        _sig(L, "pmc_slab_ipc_handle", i32, _vp, _vp)
+        _sig(L, "pmc_slab_init_ipc", i32, _vp, i32, i32, _vp)
+        _sig(L, "pmc_device_count", i32, C.POINTER(C.c_int))
         _sig(L, "pmc_slab_exchange", i32, _vp)
         _sig(L, "pmc_slab_sweep", i32, _vp, u32)
         _sig(L, "pmc_slab_finish", i32, _vp)

@@ -21,7 +21,7 @@ from typing import Optional
 
 import numpy as np
 
-from ._lib import Params, Result, Stats, check, lib
+from ._lib import PMC_IPC_HANDLE_BYTES, Params, Result, Stats, check, lib
 
 FIX_SCALE = 2.0 ** 32
 
@@ -173,6 +173,20 @@ class PmcContext:
     def slab_init_local(self, rank: int, group: "LocalGroup") -> None:
         """pmc_slab_init with the in-process transport (W slabs of one process, a thread per rank)."""
         check("pmc_slab_init_local", lib().pmc_slab_init_local(self._h, rank, group.handle))
+
+    def slab_ipc_handle(self) -> bytes:
+        """This rank's IPC blob (pmc_slab_ipc_handle): its symmetric buffers and flags, to gather
+        in rank order and hand to every rank's slab_init_ipc."""
+        buf = (C.c_ubyte * PMC_IPC_HANDLE_BYTES)()
+        check("pmc_slab_ipc_handle", lib().pmc_slab_ipc_handle(self._h, buf))
+        return bytes(buf)
+
+    def slab_init_ipc(self, rank: int, world: int, blobs: list) -> None:
+        """pmc_slab_init with the IPC transport (one process per rank; blobs[r] = rank r's handle)."""
+        if len(blobs) != world or any(len(b) != PMC_IPC_HANDLE_BYTES for b in blobs):
+            raise ValueError("slab_init_ipc: one PMC_IPC_HANDLE_BYTES blob per rank expected")
+        raw = (C.c_ubyte * (PMC_IPC_HANDLE_BYTES * world)).from_buffer_copy(b"".join(blobs))
+        check("pmc_slab_init_ipc", lib().pmc_slab_init_ipc(self._h, rank, world, raw))
 
     def slab_exchange(self) -> None:
         check("pmc_slab_exchange", lib().pmc_slab_exchange(self._h))
@@ -326,6 +340,13 @@ class LocalGroup:
         if getattr(self, "handle", None):
             lib().pmc_local_group_destroy(self.handle)
             self.handle = None
+
+
+def device_count() -> int:
+    """HIP devices visible to this process (pmc_device_count); PmcError PMC_ERR_NODEV if none."""
+    n = C.c_int(0)
+    check("pmc_device_count", lib().pmc_device_count(C.byref(n)))
+    return n.value
 
 
 def comm_unique_id() -> bytes:

@@ -388,6 +388,35 @@ class SlabSimulation:
         return self.disk[self.cur][1:-1], self.n[self.cur][1:-1]
 
 
+def _all_gather_bytes(data: bytes, world: int, group=None) -> list:
+    """Every rank's `data` (equal lengths) in rank order, over the torch.distributed group (gloo:
+    CPU tensors, nccl: device tensors)."""
+    if world == 1:
+        return [data]
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    dev = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
+    mine = torch.from_numpy(np.frombuffer(data, np.uint8).copy()).to(dev)
+    out = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(out, mine, group=group)
+    return [bytes(t.cpu().numpy().tobytes()) for t in out]
+
+
+def _all_ok(ok: bool, world: int, group=None) -> bool:
+    if world == 1:
+        return ok
+    import torch
+    import torch.distributed as dist
+    dev = "cuda" if dist.get_backend(group) == "nccl" else "cpu"
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(int(t.item()))
+
+
+TRANSPORTS = ("ipc", "rccl", "local", "auto")
+
+
 def _rccl_lib_path() -> Optional[str]:
     """The librccl torch already loaded (same soname: dlopen in C shares that instance)."""
     import torch
@@ -412,7 +441,7 @@ class SlabDriver:
     def __init__(self, cps: int, nz_local: int, rank: int, world: int, stream=None, atoms_per_rank: int = 0,
                  atoms_total: int = 0, nmax: int = 16, n_moves: int = 10, seed: int = 1234,
                  use_rccl: Optional[bool] = None, group=None, local_group=None, cps_y: int = 0,
-                 flags: int = 0, lattice_cps_z: int = 0, halo: int = 0):
+                 flags: int = 0, lattice_cps_z: int = 0, halo: int = 0, transport: Optional[str] = None):
         """local_group: a pmc_amd.engine.LocalGroup -- the in-process transport (this rank is one of
         local_group.world slab contexts of this process; construct and drive each rank from its
         own thread: the exchanges are collective).  flags: pmc_params.flags (PMC_FLAG_FULL_SHUFFLE:
@@ -420,7 +449,12 @@ class SlabDriver:
         atoms_total: the lattice of atoms_total particles over a box lattice_cps_z cells tall
         (pmc_init_lattice_planes; the config-5 weak-scaling start), else over this box.  halo: halo
         planes per side, 1 or 2 (0: PMC_SLAB_HALO, default 1; the reference-like colour order always
-        uses 1)."""
+        uses 1).  transport (one process per rank): "ipc" -- the peers' buffers mapped with
+        hipIpcOpenMemHandle, exchanges pulled by the library's own copy kernels (pmc_slab_init_ipc; also
+        several rank processes on ONE GPU, which RCCL refuses); "rccl"; "local" (world 1: periodic
+        halos by local copies); "auto" -- IPC, or RCCL on every rank if any rank cannot map its peers.
+        Default: PMC_SLAB_TRANSPORT, else "ipc" for world > 1, "local" for one rank (use_rccl=True:
+        "rccl", the one-rank RCCL rehearsal)."""
         from .engine import PmcContext, comm_unique_id
         self.g = SlabGeometry(cps, nz_local, rank, world, nmax)
         if stream is None and local_group is None:
@@ -440,10 +474,32 @@ class SlabDriver:
             if local_group.world != world:
                 raise ValueError("local_group.world != world")
             self.ctx.slab_init_local(rank, local_group)
+            self.transport = "in-process"
         else:
-            use_rccl = world > 1 if use_rccl is None else use_rccl
+            if transport is None:
+                transport = ("rccl" if use_rccl else
+                             os.environ.get("PMC_SLAB_TRANSPORT") or ("ipc" if world > 1 else "local"))
+            if transport not in TRANSPORTS:
+                raise ValueError(f"transport must be one of {TRANSPORTS}")
+            if transport == "local" and world > 1:
+                raise ValueError("transport 'local' is a one-rank slab")
+            if transport in ("ipc", "auto"):
+                ok, err = True, None
+                try:
+                    blobs = _all_gather_bytes(self.ctx.slab_ipc_handle(), world, group)
+                    self.ctx.slab_init_ipc(rank, world, blobs)
+                except Exception as e:      # (collective below: every rank learns of a failure)
+                    ok, err = False, e
+                if _all_ok(ok, world, group):
+                    transport = "ipc"
+                elif transport == "ipc":
+                    raise RuntimeError(f"IPC halo transport unavailable on rank {rank}: {err!r}") if err \
+                        else RuntimeError("IPC halo transport unavailable on another rank")
+                else:
+                    transport = "rccl"      # auto: every rank falls back together
+            self.transport = transport
             uid = None
-            if use_rccl:
+            if transport == "rccl":
                 import torch
                 lib_path = _rccl_lib_path()
                 if lib_path and not os.environ.get("PMC_RCCL_LIB"):
@@ -457,7 +513,8 @@ class SlabDriver:
                     dist.broadcast(on, src=0, group=group)
                     buf = on.cpu()
                 uid = bytes(buf.numpy().tobytes())
-            self.ctx.slab_init(rank, world, uid)      # RCCL communicator: collective over the ranks
+            if transport != "ipc":
+                self.ctx.slab_init(rank, world, uid)  # RCCL communicator: collective over the ranks
         if atoms_total and lattice_cps_z:
             self.ctx.init_lattice_planes(atoms_total, lattice_cps_z)
             self.ctx.slab_exchange()

@@ -1,0 +1,70 @@
+#!/bin/bash
+# Parameterised GPU-box measurement steps (replaces the one-off rNNx.sh wrappers).
+#   bash tools/steps.sh TAG STEP [STEP ...]
+# Every step runs under its own time limit; the script stops at the first failing step (no retries).
+# Output: gpurun_out/TAG/<step>.log (+ JSON lines of bench steps in <step>.json).
+# Steps:
+#   tests            the whole -m gpu suite
+#   tests:<pattern>  pytest -m gpu -k <pattern>
+#   mp               tests/test_gpu_multiprocess.py (rank processes over the IPC transport)
+#   smoke            __graft_entry__.smoke()
+#   bench            default bench line (config 3, the driver's --steps 20 --warmup 5)
+#   bench2           config 2
+#   slab1            config 3 through the slab driver, one rank, local halos
+#   emu<R>[-<tp>][-d<us>]   config-4 rehearsal of R ranks (one rank's slab), transport tp (local|ipc|rccl,
+#                    default local), injected exchange delay us
+#   mp2bench         bench.py --gpus 2 --same-device --config 4 (rank processes, IPC)
+#   rocprof          rocprofv3 --kernel-trace --stats of the default bench command
+set -o pipefail
+TAG=${1:?tag}; shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+PYT="python -u -m pytest -x -q --timeout 180 --timeout-method thread"
+summ() {   # one-line summary of a bench JSON line
+    python3 - "$1" <<'EOF'
+import json, sys
+for ln in open(sys.argv[1]):
+    if ln.startswith("{"):
+        d = json.loads(ln); r = d.get("roofline") or {}; p = d.get("parity") or {}
+        print("%s value %.4g ms/step %.4f launch %s shift %s frac %s parity %s/%s" % (
+            sys.argv[1].split("/")[-1], d["value"], d["ms_per_step"],
+            "%.4f" % r["launch_ms"] if r.get("launch_ms") else None,
+            "%.4f" % r["shift_ms"] if r.get("shift_ms") else None,
+            "%.4f" % r["frac"] if r.get("frac") else None,
+            p.get("state_bitwise_equal"), p.get("counters_equal")))
+EOF
+}
+for step in "$@"; do
+    log=$OUT/${step//[:\/]/_}.log
+    echo "== $step"
+    case $step in
+        tests) timeout -k 10 900 $PYT tests -m gpu > $log 2>&1 ;;
+        tests:*) timeout -k 10 600 $PYT tests -m gpu -k "${step#tests:}" > $log 2>&1 ;;
+        mp) timeout -k 10 600 $PYT tests/test_gpu_multiprocess.py -m gpu > $log 2>&1 ;;
+        smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $log 2>&1 ;;
+        bench) timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $log 2>&1 ;;
+        bench2) timeout -k 10 300 python bench.py --config 2 --steps 160 --warmup 8 > $log 2>&1 ;;
+        slab1) timeout -k 10 300 python bench.py --slab --no-cpu-baseline --steps 20 --warmup 5 > $log 2>&1 ;;
+        emu*)
+            spec=${step#emu}; R=${spec%%-*}; tp=local; dl=0
+            IFS=- read -ra parts <<< "$spec"
+            for p in "${parts[@]:1}"; do
+                case $p in d*) dl=${p#d} ;; *) tp=$p ;; esac
+            done
+            timeout -k 10 300 python bench.py --config 4 --emulate-ranks $R --transport $tp --xfer-delay-us $dl \
+                --no-cpu-baseline --steps 100 --warmup 20 > $log 2>&1 ;;
+        mp2bench) timeout -k 10 400 python bench.py --gpus 2 --same-device --config 4 --steps 20 --warmup 5 \
+                --rank-timeout 360 > $log 2>&1 ;;
+        rocprof) (cd /tmp && export TMPDIR=/tmp) ; timeout -k 10 400 rocprofv3 --kernel-trace --stats \
+                -d $OUT/rocprof -o bench -- python3 bench.py --steps 20 --warmup 5 > $log 2>&1 ;;
+        *) echo "unknown step $step"; exit 2 ;;
+    esac
+    rc=$?
+    if [ $rc -ne 0 ]; then echo "step $step failed rc $rc"; tail -40 $log; exit $rc; fi
+    case $step in
+        tests*|mp) tail -1 $log ;;
+        smoke) tail -1 $log ;;
+        rocprof) grep '^{' $log > $OUT/${step}.json; summ $OUT/${step}.json ;;
+        *) grep '^{' $log > $OUT/${step//[:\/]/_}.json; summ $OUT/${step//[:\/]/_}.json ;;
+    esac
+done
