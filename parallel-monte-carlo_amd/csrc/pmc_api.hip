@@ -5,6 +5,7 @@
 // is asynchronous on the context stream; only the *_read / copy / synchronize calls block.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
@@ -1071,10 +1072,16 @@ struct pmc_slab {
     };
     std::vector<IpcPeer> peers;
     uint64_t ipc_timeout = 0;             // wait limit, ticks of the 100 MHz real-time counter
+    // the latest exchange whose readers may still be pulling from this rank's buffers: the next
+    // exchange waits for their "pulled" (so does ipc_settle, before host-visible points)
+    uint64_t pend_seq = 0;
+    std::vector<int> pend_readers;
     bool messages() const { return comm != nullptr || group != nullptr || ipc; }
 };
 
 namespace {
+
+int ipc_settle(pmc_ctx* c);   // IPC transport: wait for the latest exchange's readers (on aux)
 
 bool slab_is_ipc(const pmc_ctx* c) { return c->slab && c->slab->ipc; }
 int slab_pending_zdir(const pmc_ctx* c) { return c->slab ? c->slab->pending_zdir : 0; }
@@ -1082,6 +1089,7 @@ int slab_pending_zdir(const pmc_ctx* c) { return c->slab ? c->slab->pending_zdir
 void drop_slab(pmc_ctx* c) {
     pmc_slab* s = c->slab;
     if (!s) return;
+    (void)ipc_settle(c);   // (IPC: no peer still pulls from the buffers about to be freed)
     if (s->aux) (void)hipStreamSynchronize(s->aux);
     if (s->comm && rccl().ok) (void)rccl().comm_destroy(s->comm);
     if (s->group) {
@@ -1143,6 +1151,7 @@ int slab_split(int chains, int nz, int zs[4]) {
 int slab_join(pmc_ctx* c) {
     pmc_slab* s = c->slab;
     if (!s) return PMC_OK;
+    if (int rc = ipc_settle(c)) return rc;   // IPC: the peers are done reading this rank's buffers
     for (hipStream_t st : {s->aux, s->hi[0], s->hi[1], s->hr}) {
         if (!st) continue;
         hipError_t e = hipEventRecord(s->ev_b, st);
@@ -1195,33 +1204,62 @@ int xfer_seg(XferCopy& cp, const void* src, void* dst, size_t bytes) {
     return PMC_OK;
 }
 
-void xfer_flag_add(XferFlags& w, const uint64_t* f) {
+void xfer_flag_add(XferFlags& w, const uint64_t* f, uint64_t target) {
     for (int i = 0; i < w.n; ++i)
-        if (w.flag[i] == f) return;
-    w.flag[w.n++] = f;
+        if (w.flag[i] == f) {
+            if (target > w.target[i]) w.target[i] = target;
+            return;
+        }
+    w.flag[w.n] = f;
+    w.target[w.n++] = target;
 }
 
-// exchange k over IPC: ready[me] = k and wait for the senders' ready; pull every message from the
-// peer's buffer (the copy kernel's last block stores pulled[me] = k); wait for the readers' pulled
-// before the exchange stream may overwrite this rank's buffers again.  Three launches on aux.
+const uint64_t* ipc_peer_flags(const pmc_slab* s, int p) {
+    return reinterpret_cast<const uint64_t*>(s->peers[(size_t)p].base[kIpcBufs - 1]);
+}
+
+// the waits on the previous exchange's readers (pulled >= its sequence number), then none pending
+void ipc_take_pending(pmc_slab* s, XferFlags& w) {
+    for (int p : s->pend_readers) xfer_flag_add(w, ipc_peer_flags(s, p) + kFlagPulled, s->pend_seq);
+    s->pend_readers.clear();
+    s->pend_seq = 0;
+}
+
+// exchange k over IPC: ONE launch on aux (k_xfer): ready[me] = k; wait for the senders' ready >= k
+// and for the previous exchange's readers' pulled; pull every message from the peer's buffer; the
+// last block stores pulled[me] = k.  This exchange's readers are waited for by the next exchange or
+// by ipc_settle, whichever comes first: nothing before either overwrites what they read (the sent
+// planes of buffer cur are rewritten only by a later sweep's shift, after more exchanges).
 int ipc_run(pmc_ctx* c, const std::vector<XferMsg>& sends, const std::vector<XferMsg>& recvs) {
     pmc_slab* s = c->slab;
     const uint64_t seq = ++c->xseq;
-    XferFlags wr{}, wp{};
+    XferFlags w{};
     XferCopy cp{};
-    auto pflags = [&](int p) { return reinterpret_cast<const uint64_t*>(s->peers[(size_t)p].base[kIpcBufs - 1]); };
+    ipc_take_pending(s, w);
     for (const XferMsg& m : recvs) {
         const void* src = m.sym ? ipc_translate(c, s, m.peer, m.sym, m.bytes) : nullptr;
         if (!src) return fail(PMC_ERR_ARG, "IPC transport: a receive's source is not in a symmetric buffer");
         if (int rc = xfer_seg(cp, src, m.buf, m.bytes)) return rc;
-        xfer_flag_add(wr, pflags(m.peer) + kFlagReady);
+        xfer_flag_add(w, ipc_peer_flags(s, m.peer) + kFlagReady, seq);
     }
-    for (const XferMsg& m : sends) xfer_flag_add(wp, pflags(m.peer) + kFlagPulled);
-    hipError_t e = launch_xfer_flag(c->xflags + kFlagReady, seq, wr, s->ipc_timeout, c->flags, s->aux);
-    if (e == hipSuccess)
-        e = launch_xfer_copy(cp, c->xflags + kFlagPulled, seq, reinterpret_cast<unsigned*>(c->xflags + kFlagDone), s->aux);
-    if (e == hipSuccess) e = launch_xfer_flag(nullptr, seq, wp, s->ipc_timeout, c->flags, s->aux);
+    for (const XferMsg& m : sends)
+        if (std::find(s->pend_readers.begin(), s->pend_readers.end(), m.peer) == s->pend_readers.end())
+            s->pend_readers.push_back(m.peer);
+    s->pend_seq = seq;
+    hipError_t e = launch_xfer(cp, w, c->xflags + kFlagReady, c->xflags + kFlagPulled, seq,
+                               reinterpret_cast<unsigned*>(c->xflags + kFlagDone), s->ipc_timeout, c->flags, s->aux);
     return e == hipSuccess ? PMC_OK : hip_fail(e, "IPC halo exchange");
+}
+
+// the readers of the latest exchange are done (a wait launch on aux) -- before the host or the
+// context stream may read or overwrite this rank's buffers, and before teardown
+int ipc_settle(pmc_ctx* c) {
+    pmc_slab* s = c->slab;
+    if (!s || !s->ipc || s->pend_readers.empty()) return PMC_OK;
+    XferFlags w{};
+    ipc_take_pending(s, w);
+    hipError_t e = launch_xfer_flag(nullptr, 0, w, s->ipc_timeout, c->flags, s->aux);
+    return e == hipSuccess ? PMC_OK : hip_fail(e, "IPC settle");
 }
 
 // carry the queued messages on the aux stream (RCCL group, IPC pulls, or the in-process group's copies)
@@ -1427,7 +1465,11 @@ int slab_flush_z(pmc_ctx* c) {
     if (!s || !s->pending_zdir) return PMC_OK;
     const int dir = s->pending_zdir;
     s->pending_zdir = 0;
-    return slab_exchange_zplane(c, dir);
+    if (int rc = slab_exchange_zplane(c, dir)) return rc;
+    // IPC: the plane it sent may be the next run's boundary plane (rewritten in place before any
+    // later exchange waits for this one's readers): settle now -- this path is off the sweep's
+    // critical path (a flush before a non-consecutive sweep or a host-visible call)
+    return ipc_settle(c);
 }
 
 }  // namespace
@@ -1768,6 +1810,9 @@ int pmc_slab_exchange(pmc_ctx* c) {
     for (hipStream_t h : {s->hi[0], s->hi[1], s->hr})
         if (h) PMC_HIP(hipStreamWaitEvent(h, s->ev_i, 0));
     if ((rc = slab_exchange_full(c))) return rc;
+    // IPC: the sent planes are rewritten in place by the next sweep's first runs (boundary and, with
+    // two-plane halos, interior chains on other streams) before any later exchange: settle now
+    if ((rc = ipc_settle(c))) return rc;
     PMC_HIP(hipEventRecord(s->ev_t, s->aux));
     PMC_HIP(hipStreamWaitEvent(c->stream, s->ev_t, 0));
     for (hipStream_t h : {s->hi[0], s->hi[1], s->hr})
@@ -1917,7 +1962,8 @@ int slab_sweep_h2(pmc_ctx* c, uint32_t sweep) {
     }
     // the send planes: shiftCells of planes [0, 2) and [nz-2, nz) again, into the send buffer (the
     // kernel addresses its output by storage plane: the base is offset so plane 0 / nz-2 lands at
-    // the buffer's start / third plane)
+    // the buffer's start / third plane) -- IPC: after the previous sweep's readers pulled from it
+    if ((rc = ipc_settle(c))) return rc;
     {
         const int h = c->P.halo;
         const ptrdiff_t pf = (ptrdiff_t)plane_floats(c), pc = (ptrdiff_t)plane_cells(c);
@@ -2243,22 +2289,23 @@ int pmc_slab_observables(pmc_ctx* c, int with_energy, pmc_stats* out, double* e_
     } else if (s->ipc) {
         // every rank's five sums into its flags buffer; each rank pulls all of them (one exchange:
         // ready, pull, pulled -- the sequence numbers of the halo exchanges continue)
+        if (int rc = ipc_settle(c)) return rc;     // (nobody still reads the reduction slot)
         const uint64_t seq = ++c->xseq;
-        XferFlags wr{}, wp{};
+        XferFlags w{};
         XferCopy cp{};
         for (int p = 0; p < s->world; ++p) {
-            const uint64_t* pf = reinterpret_cast<const uint64_t*>(s->peers[(size_t)p].base[kIpcBufs - 1]);
+            const uint64_t* pf = ipc_peer_flags(s, p);
             if (int rc = xfer_seg(cp, pf + kFlagRed, c->xflags + kFlagGather + 8 * p, sizeof v)) return rc;
             if (p != s->rank) {
-                xfer_flag_add(wr, pf + kFlagReady);
-                xfer_flag_add(wp, pf + kFlagPulled);
+                xfer_flag_add(w, pf + kFlagReady, seq);
+                s->pend_readers.push_back(p);
             }
         }
+        s->pend_seq = seq;
         PMC_HIP(hipMemcpyAsync(c->xflags + kFlagRed, v, sizeof v, hipMemcpyHostToDevice, s->aux));
-        PMC_HIP(launch_xfer_flag(c->xflags + kFlagReady, seq, wr, s->ipc_timeout, c->flags, s->aux));
-        PMC_HIP(launch_xfer_copy(cp, c->xflags + kFlagPulled, seq, reinterpret_cast<unsigned*>(c->xflags + kFlagDone),
-                                 s->aux));
-        PMC_HIP(launch_xfer_flag(nullptr, seq, wp, s->ipc_timeout, c->flags, s->aux));
+        PMC_HIP(launch_xfer(cp, w, c->xflags + kFlagReady, c->xflags + kFlagPulled, seq,
+                            reinterpret_cast<unsigned*>(c->xflags + kFlagDone), s->ipc_timeout, c->flags, s->aux));
+        if (int rc = ipc_settle(c)) return rc;
         std::vector<uint64_t> h((size_t)8 * s->world);
         PMC_HIP(hipMemcpyAsync(h.data(), c->xflags + kFlagGather, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost,
                                s->aux));

@@ -149,6 +149,7 @@ hipError_t launch_spin(double us, hipStream_t st);
 constexpr int kXferMax = 16;       // flags waited on / segments copied per launch (peers <= 16)
 struct XferFlags {
     const uint64_t* flag[kXferMax];
+    uint64_t target[kXferMax];     // wait until *flag[i] >= target[i]
     int n;
 };
 struct XferSeg {
@@ -161,11 +162,13 @@ struct XferCopy {
     XferSeg seg[kXferMax];
     int n;
 };
-// mine (may be null) := seq, then wait until every w.flag[i] >= seq (timeout: error flag 512)
+// mine (may be null) := seq, then wait until every w.flag[i] >= w.target[i] (timeout: error flag 512)
 hipError_t launch_xfer_flag(uint64_t* mine, uint64_t seq, const XferFlags& w, uint64_t timeout_ticks, uint32_t* err,
                             hipStream_t st);
-// copy every segment; the last block stores *pulled = seq (pulled may be null: no signal)
-hipError_t launch_xfer_copy(const XferCopy& cp, uint64_t* pulled, uint64_t seq, unsigned* done, hipStream_t st);
+// one exchange (two launches): *ready := seq and wait for w; then copy every segment, the last block
+// storing *pulled = seq
+hipError_t launch_xfer(const XferCopy& cp, const XferFlags& w, uint64_t* ready, uint64_t* pulled, uint64_t seq,
+                       unsigned* done, uint64_t timeout_ticks, uint32_t* err, hipStream_t st);
 hipError_t launch_selftest(const uint32_t* words, int count, float* out_f, double* out_d,
                            float rc2, hipStream_t st);
 

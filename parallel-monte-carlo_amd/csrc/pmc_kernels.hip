@@ -2520,18 +2520,21 @@ hipError_t launch_spin(double us, hipStream_t st) {
 // IPC halo transport (pmc_slab_init_ipc): the slab driver's point-to-point messages between rank
 // processes of one node (or several processes on one GPU), through IPC-mapped peer buffers and
 // per-rank sequence flags in uncached device memory -- no host round trip per exchange.  Exchange k
-// on the exchange stream is three launches:
-//   k_xfer_flag (signal + wait): ready[me] = k, then wait until ready[p] >= k for every peer p this
-//     rank receives from (their send planes are complete: stream order on their side);
-//   k_xfer_copy: pull every message from the peer's buffer into ours, grid-wide; the last block
-//     to finish stores pulled[me] = k (every read of the peers' buffers is done);
-//   k_xfer_flag (wait only): until pulled[p] >= k for every peer p that reads our buffers, so the
-//     exchange stream's later work may overwrite them.
-// The copy is a separate launch from the wait on purpose: it starts after the wait kernel has
-// completed, so the kernel-start acquire the command processor performs orders its reads after
-// the peers' kernel-end releases, exactly as a cross-stream event wait would (no in-kernel cache
-// maintenance on peer data).  Waits give up after `timeout` ticks of the 100 MHz real-time
-// counter and set error-flag bit 9 (value 512) instead of hanging the GPU.
+// on the exchange stream is two launches:
+//   k_xfer_flag: ready[me] = k (every earlier kernel of the stream has ended: its writes are
+//     released); then wait until ready[p] >= k for each peer p this rank receives from, and until
+//     pulled[p] >= k' for each peer that read this rank's buffers in the previous exchange k' (so
+//     this exchange's copies and everything after it may overwrite them);
+//   k_xfer: pull every message from the peer's buffer into ours, grid-wide; the last block to
+//     finish stores pulled[me] = k.
+// The copy is its own launch, after the wait kernel has completed: the kernel-start acquire the
+// command processor performs then orders its reads after the peers' kernel-end releases, exactly as
+// a cross-stream event wait would; no shader-side cache maintenance on the peer's data is relied on
+// (the AMDGPU memory model's acquire invalidates only non-local L2 lines, and what an IPC mapping of
+// a same-device peer's buffer counts as is not specified).  k_xfer_flag alone (no signal) settles the last
+// exchange's "pulled" before host-visible points (pmc_slab_finish, copies, teardown).  Waits give up
+// after `timeout` ticks of the 100 MHz real-time counter and set error-flag bit 9 (value 512)
+// instead of hanging the GPU.
 // ------------------------------------------------------------------------------------------
 namespace {
 
@@ -2543,20 +2546,26 @@ __device__ __forceinline__ void flag_store(uint64_t* p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ void __launch_bounds__(kWave) k_xfer_flag(uint64_t* mine, uint64_t seq, XferFlags w, uint64_t timeout,
-                                                      uint32_t* err) {
-    if (threadIdx.x != 0) return;
-    if (mine) flag_store(mine, seq);
+// one thread: every w.flag[i] >= w.target[i] (false on timeout, after setting error bit 9)
+__device__ __forceinline__ bool flags_wait(const XferFlags& w, uint64_t timeout, uint32_t* err) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (int i = 0; i < w.n; ++i) {
-        while (flag_load(w.flag[i]) < seq) {
+        while (flag_load(w.flag[i]) < w.target[i]) {
             if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
                 atomicOr(err, 512u);
-                return;
+                return false;
             }
             __builtin_amdgcn_s_sleep(2);
         }
     }
+    return true;
+}
+
+__global__ void __launch_bounds__(kWave) k_xfer_flag(uint64_t* mine, uint64_t seq, XferFlags w, uint64_t timeout,
+                                                      uint32_t* err) {
+    if (threadIdx.x != 0) return;
+    if (mine) flag_store(mine, seq);
+    (void)flags_wait(w, timeout, err);
 }
 
 template <class U>
@@ -2577,7 +2586,7 @@ __device__ __forceinline__ void xfer_units(const XferSeg& s, int shift) {
     for (; i < n; i += stride) dst[i] = src[i];
 }
 
-__global__ void __launch_bounds__(256) k_xfer_copy(XferCopy cp, uint64_t* pulled, uint64_t seq, unsigned* done) {
+__global__ void __launch_bounds__(256) k_xfer(XferCopy cp, uint64_t* pulled, uint64_t seq, unsigned* done) {
     for (int k = 0; k < cp.n; ++k) {
         const XferSeg& s = cp.seg[k];
         switch (s.shift) {
@@ -2588,7 +2597,6 @@ __global__ void __launch_bounds__(256) k_xfer_copy(XferCopy cp, uint64_t* pulled
             default: xfer_units<uint8_t>(s, 0); break;
         }
     }
-    if (!pulled) return;
     __syncthreads();                      // every load of this block has returned (its stores used them)
     if (threadIdx.x == 0) {
         const unsigned prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -2603,13 +2611,15 @@ __global__ void __launch_bounds__(256) k_xfer_copy(XferCopy cp, uint64_t* pulled
 
 hipError_t launch_xfer_flag(uint64_t* mine, uint64_t seq, const XferFlags& w, uint64_t timeout_ticks, uint32_t* err,
                             hipStream_t st) {
-    if (w.n < 0 || w.n > kXferMax) return hipErrorInvalidValue;
+    if (w.n < 0 || w.n > kXferMax) return hipErrorInvalidValue;   // (seq: the value stored to mine)
     hipLaunchKernelGGL(k_xfer_flag, dim3(1), dim3(kWave), 0, st, mine, seq, w, timeout_ticks, err);
     return hipGetLastError();
 }
 
-hipError_t launch_xfer_copy(const XferCopy& cp, uint64_t* pulled, uint64_t seq, unsigned* done, hipStream_t st) {
-    if (cp.n < 0 || cp.n > kXferMax) return hipErrorInvalidValue;
+hipError_t launch_xfer(const XferCopy& cp, const XferFlags& w, uint64_t* ready, uint64_t* pulled, uint64_t seq,
+                       unsigned* done, uint64_t timeout_ticks, uint32_t* err, hipStream_t st) {
+    if (cp.n < 0 || cp.n > kXferMax || w.n < 0 || w.n > kXferMax || !ready || !pulled || !done)
+        return hipErrorInvalidValue;
     uint64_t units = 0;   // 16-B units of the largest segment set the grid: ~4 per lane
     for (int k = 0; k < cp.n; ++k) {
         const XferSeg& s = cp.seg[k];
@@ -2618,9 +2628,10 @@ hipError_t launch_xfer_copy(const XferCopy& cp, uint64_t* pulled, uint64_t seq, 
             return hipErrorInvalidValue;
         units += (s.bytes + 15) / 16;
     }
+    hipLaunchKernelGGL(k_xfer_flag, dim3(1), dim3(kWave), 0, st, ready, seq, w, timeout_ticks, err);
     const uint64_t want = (units + 1023) / 1024;
-    const unsigned blocks = (unsigned)(want < 1 ? 1 : want > 512 ? 512 : want);
-    hipLaunchKernelGGL(k_xfer_copy, dim3(blocks), dim3(256), 0, st, cp, pulled, seq, done);
+    const unsigned blocks = (unsigned)(want < 1 ? 1 : want > 256 ? 256 : want);
+    hipLaunchKernelGGL(k_xfer, dim3(blocks), dim3(256), 0, st, cp, pulled, seq, done);
     return hipGetLastError();
 }
 
