@@ -41,7 +41,6 @@ struct pmc_ctx {
     int* ovf_aux = nullptr;                // second queue: launches on a caller stream (pmc_phase_range_on)
     int* ovf_b = nullptr;                  // third queue: the slab driver's boundary chain
     int* ovf_aux2 = nullptr;               // fourth queue: the slab driver's third interior chain
-    unsigned* run_ctl = nullptr;           // k_subsweep_run's claim heads and row counters (PMC_SLAB_RUNK)
     size_t ovf_bytes = 0;
     // two-plane halos: the shifted send planes (planes 0, 1 then nz-2, nz-1, with their counts)
     float* send_d = nullptr;
@@ -302,7 +301,6 @@ void pmc_destroy(pmc_ctx* c) {
     if (c->ovf_aux) (void)hipFree(c->ovf_aux);
     if (c->ovf_b) (void)hipFree(c->ovf_b);
     if (c->ovf_aux2) (void)hipFree(c->ovf_aux2);
-    if (c->run_ctl) (void)hipFree(c->run_ctl);
     for (void* m : {(void*)c->send_d, (void*)c->send_n, (void*)c->xflags})
         if (m) (void)hipFree(m);
     if (c->tmp_cnt) (void)hipFree(c->tmp_cnt);
@@ -1051,10 +1049,9 @@ struct pmc_slab {
         return v;
     }
     std::vector<XferMsg> sends, recvs;    // the exchange being assembled
-    // two-plane halos (pmc_params.halo = 2, slab_sweep_h2): the stream that visits the neighbour's
-    // boundary plane redundantly ("R"), the shifted send planes (planes 0, 1 then nz-2, nz-1, with
-    // their counts) and the counters those redundant visits add to (never read)
-    hipStream_t hr = nullptr;
+    // two-plane halos (pmc_params.halo = 2, slab_sweep_h2): the shifted send planes (the context's:
+    // planes 0, 1 then nz-2, nz-1, with their counts) and the counters the redundant visits of the
+    // neighbour's boundary plane add to (never read)
     float* send_d = nullptr;
     int16_t* send_n = nullptr;
     unsigned long long* stats_scratch = nullptr;
@@ -1099,10 +1096,6 @@ void drop_slab(pmc_ctx* c) {
     if (s->aux) (void)hipStreamDestroy(s->aux);
     for (hipStream_t h : s->hi)
         if (h) (void)hipStreamSynchronize(h);
-    if (s->hr) {
-        (void)hipStreamSynchronize(s->hr);
-        (void)hipStreamDestroy(s->hr);
-    }
     if (s->stats_scratch) (void)hipFree(s->stats_scratch);   // (the send planes are the context's)
     for (pmc_slab::IpcPeer& pr : s->peers)
         for (void* m : pr.opened) (void)hipIpcCloseMemHandle(m);
@@ -1120,15 +1113,6 @@ void drop_slab(pmc_ctx* c) {
 // interior [1, nz-1); every inner border is even (a parity-q run of a chain then ends at the same
 // side of each border).  Two chains split at 2*(nz/4), three at the even planes nearest 1/3 and
 // 2/3 of the interior; degenerate splits of thin slabs fold into fewer chains.  Returns the count.
-// PMC_SLAB_RUNK=1: each run's interior planes as ONE dataflow launch (k_subsweep_run) instead of
-// per-phase launches in interior chains
-bool slab_runk() {
-    static const bool on = [] {
-        const char* v = std::getenv("PMC_SLAB_RUNK");
-        return v && std::atoi(v) == 1;
-    }();
-    return on;
-}
 
 int slab_split(int chains, int nz, int zs[4]) {
     zs[0] = 1;
@@ -1152,7 +1136,7 @@ int slab_join(pmc_ctx* c) {
     pmc_slab* s = c->slab;
     if (!s) return PMC_OK;
     if (int rc = ipc_settle(c)) return rc;   // IPC: the peers are done reading this rank's buffers
-    for (hipStream_t st : {s->aux, s->hi[0], s->hi[1], s->hr}) {
+    for (hipStream_t st : {s->aux, s->hi[0], s->hi[1]}) {
         if (!st) continue;
         hipError_t e = hipEventRecord(s->ev_b, st);
         if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, s->ev_b, 0);
@@ -1536,13 +1520,9 @@ int slab_attach(pmc_ctx* c, int rank, int world, bool messages) {
         }();
         s->chains = forced >= 1 && forced <= 3 ? forced : 2;
     }
-    // two-plane halos: at most 2 interior chains -- the redundant halo plane takes the fourth stream
+    // two-plane halos: at most 2 interior chains
     if (c->P.halo == 2) {
         if (s->chains > 2) s->chains = 2;
-        if ((e = hipStreamCreateWithPriority(&s->hr, hipStreamNonBlocking, prio ? hi_p : 0)) != hipSuccess) {
-            drop_slab(c);
-            return hip_fail(e, "hipStreamCreate");
-        }
         const size_t sb = sizeof(unsigned long long) * kStatCounters * kStatSlots;
         if ((e = ensure_send_planes(c)) != hipSuccess || (e = hipMalloc(&s->stats_scratch, sb)) != hipSuccess ||
             (e = hipMemsetAsync(s->stats_scratch, 0, sb, c->stream)) != hipSuccess) {
@@ -1807,7 +1787,7 @@ int pmc_slab_exchange(pmc_ctx* c) {
     if (rc) return rc;
     PMC_HIP(hipEventRecord(s->ev_i, c->stream));
     PMC_HIP(hipStreamWaitEvent(s->aux, s->ev_i, 0));
-    for (hipStream_t h : {s->hi[0], s->hi[1], s->hr})
+    for (hipStream_t h : {s->hi[0], s->hi[1]})
         if (h) PMC_HIP(hipStreamWaitEvent(h, s->ev_i, 0));
     if ((rc = slab_exchange_full(c))) return rc;
     // IPC: the sent planes are rewritten in place by the next sweep's first runs (boundary and, with
@@ -1815,7 +1795,7 @@ int pmc_slab_exchange(pmc_ctx* c) {
     if ((rc = ipc_settle(c))) return rc;
     PMC_HIP(hipEventRecord(s->ev_t, s->aux));
     PMC_HIP(hipStreamWaitEvent(c->stream, s->ev_t, 0));
-    for (hipStream_t h : {s->hi[0], s->hi[1], s->hr})
+    for (hipStream_t h : {s->hi[0], s->hi[1]})
         if (h) PMC_HIP(hipStreamWaitEvent(h, s->ev_t, 0));
     PMC_HIP(hipEventRecord(s->ev_x, s->aux));
     for (hipEvent_t* ev : s->run_events()) PMC_HIP(hipEventRecord(*ev, s->aux));
@@ -1829,7 +1809,8 @@ namespace {
 // Two-plane halos (pmc_params.halo = 2): ONE exchange per sweep, after shiftCells, instead of one
 // per run.  A rank stores two halo planes on each side.  In a sweep's first run (parity a) the
 // halo plane of parity a -- the neighbour's boundary plane P_a, top halo nz for a = 0, bottom halo
-// -1 for a = 1 -- is visited here as well, redundantly, on its own stream R: its cells read only
+// -1 for a = 1 -- is visited here as well, redundantly, in the same launches as our boundary plane
+// P_a on T (k_subsweep_direct2: the two planes lie at opposite faces): its cells read only
 // our boundary plane and the second halo plane beyond it, which no phase of that run changes, and
 // its random numbers, cell centre and staging are the owner's (global cell ids), so the result is
 // the owner's bit for bit (its counters go to a scratch buffer: the owner counts them).  The second
@@ -1840,11 +1821,11 @@ namespace {
 // shifts the plane that reads it.  T also shifts the four planes the neighbours need (0, 1, nz-2,
 // nz-1) into a send buffer -- the interior chains may rewrite planes 1 and nz-2 while the exchange
 // is in flight -- and exchanges all four halo planes with their counts.  The next sweep's interior
-// chains read no halo, so they start right after the shift; only T (its boundary plane) and R (the
-// halo plane) wait for the exchange.  Streams: S + one interior stream, T, R (4 hardware queues).
+// chains read no halo, so they start right after the shift; only T (its boundary and halo planes)
+// waits for the exchange.  Streams: S + one interior stream, T.
 int slab_sweep_h2(pmc_ctx* c, uint32_t sweep) {
     pmc_slab* s = c->slab;
-    hipStream_t S = c->stream, T = s->aux, R = s->hr;
+    hipStream_t S = c->stream, T = s->aux;
     const int nz = c->P.nz_local;
     int zs[4];
     const int nc = slab_split(s->chains, nz, zs);   // <= 2 chains
@@ -1855,9 +1836,9 @@ int slab_sweep_h2(pmc_ctx* c, uint32_t sweep) {
     for (int k = 1; k < 8; ++k)
         if (plan.order[k] % 2 != (k < 4 ? a : b))
             return fail(PMC_ERR_ARG, "two-plane halos need the grouped colour order (two runs per sweep)");
-    constexpr int kB = pmc_slab::kB, kR = 2;             // ev_run rows: chains 0-1, R, T
+    constexpr int kB = pmc_slab::kB, kR = 2;             // ev_run rows: chains 0-1, the halo plane, T
     const int pa = a == 0 ? 0 : nz - 1, pb = b == 0 ? 0 : nz - 1;   // boundary planes of the runs
-    const int za = a == 0 ? nz : -1;                     // the halo plane R visits in run a
+    const int za = a == 0 ? nz : -1;                     // the halo plane T also visits in run a
     auto phases = [&](hipStream_t st, int* ovf, unsigned long long* stats, int z0, int z1, int k0, int k1,
                       bool plane) -> int {
         for (int kk = k0; kk < k1; ++kk) {
@@ -1893,15 +1874,10 @@ int slab_sweep_h2(pmc_ctx* c, uint32_t sweep) {
         return PMC_OK;
     };
     int rc;
-    // PMC_SLAB_H2_MERGE (default 1): the boundary plane and the redundant halo plane of run a as ONE
-    // launch per phase on T (k_subsweep_direct2: the two planes lie at opposite faces), no R stream;
-    // 0: the halo plane on its own stream R
-    static const bool merge = [] {
-        const char* v = std::getenv("PMC_SLAB_H2_MERGE");
-        return !(v && std::atoi(v) == 0);
-    }();
-    // ---- run a: T the boundary plane, R the halo plane of parity a, the interior chains --------
-    if (merge) {
+    // ---- run a: T the boundary plane and the halo plane of parity a as ONE launch per phase
+    // (k_subsweep_direct2: the two planes lie at opposite faces), the interior chains --------------
+    // (round 4 also had the halo plane on a stream of its own: slower, removed)
+    {
         const int z0 = pa < za ? pa : za, z1 = pa < za ? za : pa;
         unsigned long long* s0 = z0 == pa ? c->stats : s->stats_scratch;
         unsigned long long* s1 = z0 == pa ? s->stats_scratch : c->stats;
@@ -1915,12 +1891,6 @@ int slab_sweep_h2(pmc_ctx* c, uint32_t sweep) {
         }
         PMC_HIP(hipEventRecord(s->ev_run[kB][a], T));
         PMC_HIP(hipEventRecord(s->ev_run[kR][a], T));      // (the halo plane is T's too)
-    } else {
-        if ((rc = phases(T, c->ovf_b, c->stats, pa, pa + 1, 0, 4, true))) return rc;
-        PMC_HIP(hipEventRecord(s->ev_run[kB][a], T));
-        PMC_HIP(hipStreamWaitEvent(R, s->ev_x, 0));     // the last exchange filled the halos R reads
-        if ((rc = phases(R, c->ovf_aux2, s->stats_scratch, za, za + 1, 0, 4, true))) return rc;
-        PMC_HIP(hipEventRecord(s->ev_run[kR][a], R));
     }
     for (int j = 0; j < nc; ++j) {
         if (zs[j + 1] > zs[j] && (rc = phases(ist[j], iovf[j], c->stats, zs[j], zs[j + 1], 0, 4, false))) return rc;
@@ -1988,7 +1958,6 @@ int slab_sweep_h2(pmc_ctx* c, uint32_t sweep) {
     PMC_HIP(hipEventRecord(s->ev_i, S));
     for (int j = 1; j < nc; ++j) PMC_HIP(hipStreamWaitEvent(ist[j], s->ev_i, 0));
     PMC_HIP(hipStreamWaitEvent(T, s->ev_i, 0));
-    PMC_HIP(hipStreamWaitEvent(R, s->ev_i, 0));
     if (stale) {
         const int zn = hp == 0 ? 1 : nz - 2;              // the owned plane next to hp
         const int j = owner(zn);
@@ -2011,13 +1980,7 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
     // (chain 0 on the context stream S); every inner border zs[j] is even, so every parity-q run
     // of a chain ends at the same side of each border
     int zs[4];
-    const bool runk = slab_runk();
-    const int nc = slab_split(runk ? 1 : s->chains, nz, zs);
-    if (runk && !c->run_ctl) {
-        const size_t nb = sizeof(unsigned) * subsweep_run_ctl_ints(c->G);
-        PMC_HIP(hipMalloc(&c->run_ctl, nb));
-        PMC_HIP(hipMemsetAsync(c->run_ctl, 0, nb, S));
-    }
+    const int nc = slab_split(s->chains, nz, zs);
     hipStream_t ist[3] = {S, s->hi[0], s->hi[1]};
     int* iovf[3] = {c->ovf, c->ovf_aux, c->ovf_aux2};
     const pmc_sweep_plan_t plan = pmc_plan_for_sweep_ex(c->P.seed, sweep, c->P.w, c->P.flags);
@@ -2117,13 +2080,7 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
             const int zb = q == 0 ? 0 : nz - 1;
             int r;
             if (!first && (r = border_waits(kB, zb, zb + 1, q, T, p))) return r;
-            // PMC_PROBE_SKIP_B=1: timing probe only (wrong results) -- the boundary chain's phase
-            // launches left out, the exchanges kept: what the boundary launches cost a rank sweep
-            static const bool skip_b = [] {
-                const char* v = std::getenv("PMC_PROBE_SKIP_B");
-                return v && std::atoi(v) == 1;
-            }();
-            if (!skip_b && (r = phases(T, c->ovf_b, zb, zb + 1, k, k1, true))) return r;
+            if ((r = phases(T, c->ovf_b, zb, zb + 1, k, k1, true))) return r;
             PMC_HIP(hipEventRecord(s->ev_run[kB][q], T));
             if ((r = slab_exchange_run(c, q, merge_z, direct_halo))) return r;
             merge_z = false;
@@ -2133,30 +2090,7 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
         if (b_first && (rc = boundary())) return rc;
         for (int j = 0; j < nc; ++j) {
             if (!first && (rc = border_waits(j, zs[j], zs[j + 1], q, ist[j], p))) return rc;
-            if (runk && j == 0) {
-                // the run's interior planes of parity q as one dataflow launch: colour planes cz with
-                // z = 2 cz + q in [1, nz-1)
-                RunDesc rd;
-                rd.nph = k1 - k;
-                rd.oz = q;
-                rd.cz0 = q == 0 ? 1 : 0;                               // (z = 0 is the boundary plane)
-                rd.ncz = nz - 2 - q >= 0 ? (nz - 2 - q) / 2 + 1 - rd.cz0 : 0;  // last z <= nz - 2
-                rd.oxy = 0;
-                for (int kk = k; kk < k1; ++kk) {
-                    int o[3];
-                    pmc_colour_offset(plan.order[kk], o);
-                    rd.oxy |= (o[0] | (o[1] << 1)) << (2 * (kk - k));
-                }
-                if (rd.ncz > 0) {
-                    hipError_t le = launch_run_check(c->G, c->run_ctl, c->ovf, c->flags, true, S);
-                    if (le == hipSuccess) {
-                        LaunchTiming lt;
-                        le = launch_subsweep_run(c->G, c->disk[c->cur], c->n[c->cur], rd, sweep, c->stats, c->ovf,
-                                                 c->run_ctl, c->flags, S, next_timing(c, 0, &lt));
-                    }
-                    if (le != hipSuccess) return hip_fail(le, "run launch");
-                }
-            } else if (zs[j + 1] > zs[j] && (rc = phases(ist[j], iovf[j], zs[j], zs[j + 1], k, k1, false))) {
+            if (zs[j + 1] > zs[j] && (rc = phases(ist[j], iovf[j], zs[j], zs[j + 1], k, k1, false))) {
                 return rc;
             }
             PMC_HIP(hipEventRecord(s->ev_run[j][q], ist[j]));
@@ -2220,7 +2154,7 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
     // After a shift along z in direction dir the halo on the +dir side is received: the neighbour's
     // new plane next to it (plane 0 of the rank above for dir > 0, its top plane nz-1 of the rank
     // below for dir < 0) -- exactly the plane that neighbour sends as the boundary plane of its
-    // run of parity 0 (dir > 0) or 1 (dir < 0) after that run.  Default (PMC_SLAB_DEFER_Z=0: off): when the next
+    // run of parity 0 (dir > 0) or 1 (dir < 0) after that run.  Default on (PMC_SLAB_DEFER_Z=0: off): when the next
     // sweep's first run is that parity, its boundary plane reads only the other halo (the
     // interior chains read none), so this exchange is skipped and the first run's exchange brings
     // the plane -- with its counts -- one run later: one exchange (xGMI latency) less on the
@@ -2245,19 +2179,15 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
 
 int pmc_slab_layout(pmc_ctx* c, int* n_chains, int borders[4]) {
     if (!c || !c->slab || !n_chains || !borders) return fail(PMC_ERR_ARG, "no slab driver (pmc_slab_init)");
-    *n_chains = slab_split(slab_runk() ? 1 : c->slab->chains, c->P.nz_local, borders);
+    // (two-plane halos run at most 2 interior chains, slab_sweep_h2)
+    *n_chains = slab_split(c->P.halo == 2 && c->slab->chains > 2 ? 2 : c->slab->chains, c->P.nz_local, borders);
     return PMC_OK;
 }
 
 int pmc_slab_finish(pmc_ctx* c) {
     if (!c || !c->slab) return fail(PMC_ERR_ARG, "no slab driver (pmc_slab_init)");
     if (int rc = slab_flush_z(c)) return rc;
-    if (int rc = slab_join(c)) return rc;
-    if (c->run_ctl) {   // the last run's checks (every item claimed, no overflowing cell)
-        hipError_t e = launch_run_check(c->G, c->run_ctl, c->ovf, c->flags, true, c->stream);
-        if (e != hipSuccess) return hip_fail(e, "run check");
-    }
-    return PMC_OK;
+    return slab_join(c);
 }
 
 int pmc_slab_observables(pmc_ctx* c, int with_energy, pmc_stats* out, double* e_out) {

@@ -110,22 +110,6 @@ int small_sweep_participants(const DevGeom& g);
 hipError_t launch_sweep_small(const DevGeom& g, float* disk0, int16_t* n0, float* disk1, int16_t* n1, int cur,
                               unsigned long long* stats, uint32_t* flags, unsigned* bar, uint64_t seed,
                               uint32_t first, int count, uint32_t plan_flags, hipStream_t st);
-// A run of colour phases of equal z parity in ONE launch (k_subsweep_run; slab interior planes):
-// nph phases (colour offsets ox, oy of phase j in bits 2j, 2j+1 of oxy; oz), colour planes [cz0, cz0 + ncz).  ctl: the run's claim
-// heads and row counters (subsweep_run_ctl_ints), zeroed by launch_run_check(reset) before every run.
-struct RunDesc {
-    int nph, oz, cz0, ncz;
-    int oxy;                       // phase j's colour offsets: ox = bit 2j, oy = bit 2j+1
-};
-// ctl layout (ints): claim head of XCD x at 32x (one 128-B line each), expected item counts at
-// [kRunCtlExp, +8), row counters from kRunCtlHead
-constexpr int kRunCtlExp = 256;
-constexpr int kRunCtlHead = 288;
-size_t subsweep_run_ctl_ints(const DevGeom& g);
-hipError_t launch_subsweep_run(const DevGeom& g, float* disk, const int16_t* n, const RunDesc& rd, uint32_t sweep,
-                               unsigned long long* stats, int* ovf, unsigned* ctl, uint32_t* flags, hipStream_t st,
-                               const LaunchTiming* tm = nullptr);
-hipError_t launch_run_check(const DevGeom& g, unsigned* ctl, int* ovf, uint32_t* flags, bool reset, hipStream_t st);
 hipError_t launch_shift(const DevGeom& g, const float* din, const int16_t* nin, float* dout,
                         int16_t* nout, int f, float d, uint32_t* flags, hipStream_t st,
                         const LaunchTiming* tm = nullptr);

@@ -154,22 +154,6 @@ template <> struct DiskAddr<0> {
     __device__ static __forceinline__ float ld(const float* b, uint32_t off) { return b[(uint64_t)off]; }
     __device__ static __forceinline__ void st(float* b, uint32_t off, float v) { b[(uint64_t)off] = v; }
 };
-// The run kernel (k_subsweep_run): 32-bit byte offsets, loads that bypass the CU's vector L1
-// (global_load ... sc1, served by the XCD's L2): rows another wave of the same XCD rewrote earlier in
-// the launch may sit stale in this CU's L1 (MI355X_MICROARCH.md, inter-workgroup visibility: the
-// L1 is never refreshed by other CUs' stores); every writer of those rows runs on the same XCD, so
-// its L2 holds them.  Stores are plain (the L1 is write-through).
-template <> struct DiskAddr<2> {
-    static constexpr uint32_t kUnit = 4;
-    __device__ static __forceinline__ float ld(const float* b, uint32_t off) {
-        // a relaxed agent-scope load: global_load_dword ... sc1 (SGPR base + VGPR offset, as the plain form)
-        const unsigned* p = (const unsigned*)((const char*)b + (uint64_t)off);
-        return __builtin_bit_cast(float, __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    }
-    __device__ static __forceinline__ void st(float* b, uint32_t off, float v) {
-        *(float*)((char*)b + (uint64_t)off) = v;
-    }
-};
 
 // Philox4x32-10 with the host-computed key schedule (bit-identical to pmc_philox4x32_10: round
 // r uses key (k0 + r*W0, k1 + r*W1)); fully unrolled, the keys are SGPR operands.
@@ -439,17 +423,10 @@ struct VisitLoads {
             vz[q] = DiskAddr<OFF32>::ld(disk, off + 2 * nm_off);
         }
         const int l = lane < nm ? lane : 0;
-        if constexpr (OFF32 == 2) {
-            const uint32_t o = (cg.c * (uint32_t)(3 * nm) + (uint32_t)l) * 4u;
-            ownx = DiskAddr<2>::ld(disk, o);
-            owny = DiskAddr<2>::ld(disk, o + nm_off);
-            ownz = DiskAddr<2>::ld(disk, o + 2 * nm_off);
-        } else {
-            const float* own = disk + (uint64_t)cg.c * (uint32_t)(3 * nm);   // wave-uniform base
-            ownx = own[l];
-            owny = own[nm + l];
-            ownz = own[2 * nm + l];
-        }
+        const float* own = disk + (uint64_t)cg.c * (uint32_t)(3 * nm);   // wave-uniform base
+        ownx = own[l];
+        owny = own[nm + l];
+        ownz = own[2 * nm + l];
     }
 };
 
@@ -1229,133 +1206,6 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_full(DevGeom g, 
                                                                  t, cz0);
 }
 
-// ------------------------------------------------------------------------------------------
-// A whole RUN of colour phases in ONE launch (k_subsweep_run; the slab driver's interior planes,
-// PMC_SLAB_RUNK=1).  In a run of equal z parity q only the parity-q planes change, each plane's
-// phases read only its own plane and the parity 1-q planes next to it, which nothing in the run
-// writes.  Inside a plane, phase j's cells read the cells their in-plane 3x3 neighbourhood holds,
-// written by the earlier phases of the run: cell (x, y) of phase j needs phase j-1 done in the
-// colour rows y-1..y+1 (earlier phases follow by induction: each of those rows waited for its own
-// neighbourhood).  So instead of a kernel boundary (and a launch tail) between phases, each wave
-// waits only for the one or two rows it reads -- dataflow, no grid barrier.
-//
-// Coherence without cross-XCD traffic: plane i of the run belongs to XCD i % 8 (XCC_ID register):
-// only waves on that XCD visit its cells, so every row a wave waits for was written by a wave of
-// the SAME XCD, through the same L2 (the L1 is write-through); the reader bypasses its CU's L1
-// (DiskAddr<2>: global_load sc1), the writer drains its stores (s_waitcnt vmcnt(0)) before it
-// counts its row done with an L2 atomic.  Work is claimed in order from a per-XCD counter
-// (dynamic: only a running wave holds an item, so the smallest unfinished item's rows are always
-// done or being visited -- no deadlock whatever the residency; one item per wave, so slots free up
-// for the boundary chain's launches as they do between ordinary launches), phase-major, rows rotated by 2 per
-// phase so that a row's dependencies were claimed about a plane-phase earlier (no waiting in the
-// steady state).  Waits give up after 0.2 s (error bit 8, value 256) instead of hanging.  A cell
-// whose filtered stencil exceeds the main capacity cannot be visited here (no fallback launch
-// between phases): it is queued in `ovf` and k_run_check raises error bit 6 (value 64) -- at the
-// configs' 4.77 particles per cell a stencil holds ~98 partners of the 224.
-// ------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t xcc_id() {
-    uint32_t x;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-    return x & 0xFu;
-}
-
-// items of XCD x: phases x its planes x colour rows x two-cell waves per row
-__device__ __forceinline__ uint32_t run_items_of(const RunDesc& rd, uint32_t x, uint32_t rows, uint32_t wpr) {
-    const uint32_t m = (uint32_t)rd.ncz > x ? ((uint32_t)rd.ncz - x + 7u) / 8u : 0u;
-    return (uint32_t)rd.nph * m * rows * wpr;
-}
-
-template <int NSLOT, int NMC>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_subsweep_run(
-    DevGeom g, float* __restrict__ disk, const int16_t* __restrict__ ncnt, RunDesc rd, uint32_t sweep,
-    unsigned long long* __restrict__ stats, int cap, int* __restrict__ ovf, unsigned* __restrict__ ctl,
-    uint32_t* __restrict__ flags) {
-    extern __shared__ __attribute__((aligned(16))) float smem[];
-    const int lane = threadIdx.x & (kWave - 1);
-    const uint32_t hx = (uint32_t)g.cps_x >> 1, rows = (uint32_t)g.cps_y >> 1;
-    const uint32_t wpr = (hx + 1u) >> 1;                      // two-cell waves per colour row
-    const uint32_t x = xcc_id();
-    if (x >= 8u) {
-        if (lane == 0) atomicOr(flags, 128u);                 // not an 8-XCD (SPX) dispatch
-        return;
-    }
-    // every wave records the expected item counts (k_run_check compares them with the heads)
-    if (lane < 8) ctl[kRunCtlExp + lane] = run_items_of(rd, (uint32_t)lane, rows, wpr);
-    const uint32_t items = run_items_of(rd, x, rows, wpr);
-    const uint32_t per_plane = rows * wpr;
-    const uint32_t m = items ? items / ((uint32_t)rd.nph * per_plane) : 0u;
-    const uint32_t per_phase = m * per_plane;
-    unsigned* const rowcnt = ctl + kRunCtlHead;
-    {
-        uint32_t c = 0;
-        // (workgroup scope: performed in the XCD's L2, where every claimant of this head and every
-        // poller of the row counters below runs; an agent-scope atomic would go past the L2 and
-        // serialise at ~90 per us per word, MI355X_MICROARCH.md 'dequeue')
-        if (lane == 0) c = __hip_atomic_fetch_add(&ctl[x * 32u], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        c = (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
-        if (c >= items) return;
-        const uint32_t j = c / per_phase, r1 = c - j * per_phase;
-        const uint32_t sp = r1 / per_plane, r2 = r1 - sp * per_plane;
-        const uint32_t rr = r2 / wpr, w = r2 - rr * wpr;
-        const uint32_t i = x + 8u * sp;                       // plane of the run (colour plane cz0 + i)
-        uint32_t tb = rr + 2u * j;                            // rows rotated by 2 per phase
-        while (tb >= rows) tb -= rows;
-        const int ox = (rd.oxy >> (2 * j)) & 1, oy = (rd.oxy >> (2 * j + 1)) & 1;
-#ifdef PMC_PROBE_RUNK_NOWAIT   // timing probe only (no dependency waits: wrong results)
-        if (false) {
-#else
-        if (j > 0) {
-#endif
-            // phase j-1's colour rows tb' with 2tb' + oy' in [y-1, y+1], y = 2tb + oy
-            const int oyp = (rd.oxy >> (2 * j - 1)) & 1;
-            uint32_t t0 = tb, t1 = tb;
-            if (oy != oyp) {
-                if (oy == 1) t1 = tb + 1u == rows ? 0u : tb + 1u;
-                else t0 = tb == 0u ? rows - 1u : tb - 1u;
-            }
-            const unsigned* base = rowcnt + ((j - 1u) * (uint32_t)rd.ncz + i) * rows;
-            const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-            while (true) {
-                const unsigned a = __hip_atomic_load(base + t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const unsigned b = __hip_atomic_load(base + t1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (__builtin_amdgcn_readfirstlane((int)(a >= wpr && b >= wpr))) break;
-                if (__builtin_amdgcn_s_memrealtime() - t_start > 20000000ull) {   // 0.2 s at 100 MHz
-                    if (lane == 0) atomicOr(flags, 256u);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-            }
-        }
-        const uint32_t pA = 2u * w + hx * tb;
-        const bool hasB = 2u * w + 1u < hx;
-#ifdef PMC_PROBE_RUNK_PLAIN   // timing probe only (L1-cached loads: may read stale rows)
-        constexpr int kAddr = 1;
-#else
-        constexpr int kAddr = 2;
-#endif
-        subsweep_pair<NSLOT, NMC, kMainCap, kAddr>(g, disk, ncnt, ox, oy, rd.oz, sweep, stats, smem, kMainCap, cap,
-                                               (int)pA, (int)pA + 1, hasB, rd.cz0 + (int)i, 0, 1, ovf);
-        // the row's written-back cells are in the XCD's L2 before the count says so
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0)
-            __hip_atomic_fetch_add(&rowcnt[(j * (uint32_t)rd.ncz + i) * rows + tb], 1u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-}
-
-// Before each run launch (and at pmc_slab_finish): check the previous run -- every XCD claimed all
-// its items (else error bit 7, value 128: an XCD without workgroups), no cell overflowed the main
-// capacity (error bit 6, value 64) -- then zero the heads, the row counters and the overflow count.
-__global__ void k_run_check(unsigned* __restrict__ ctl, int nctl, int* __restrict__ ovf, uint32_t* __restrict__ flags,
-                            int reset) {
-    const int t = (int)threadIdx.x;
-    if (t < 8 && ctl[32 * t] < ctl[kRunCtlExp + t]) atomicOr(flags, 128u);
-    if (t == 0 && ovf[kOvfCount] != 0) atomicOr(flags, 64u);
-    __syncthreads();
-    if (!reset) return;
-    for (int k = t; k < nctl; k += (int)blockDim.x) ctl[k] = 0u;
-    if (t == 0) ovf[kOvfCount] = 0;
-}
 
 // colour phases of at most this many cells use k_subsweep_full (PMC_SMALL_LAUNCH; 0 disables it).
 // Measured (profiles/r03sl_small_launch.txt): 16^3 0.122 -> 0.073 ms per sweep, 24^3 0.141 ->
@@ -3052,34 +2902,6 @@ hipError_t launch_energy(const DevGeom& g, const float* disk, const int16_t* n,
     return hipGetLastError();
 }
 
-size_t subsweep_run_ctl_ints(const DevGeom& g) {
-    return (size_t)kRunCtlHead + (size_t)4 * (size_t)(g.nz_local / 2 + 1) * (size_t)(g.cps_y / 2);
-}
-
-hipError_t launch_run_check(const DevGeom& g, unsigned* ctl, int* ovf, uint32_t* flags, bool reset, hipStream_t st) {
-    hipLaunchKernelGGL(k_run_check, dim3(1), dim3(256), 0, st, ctl, (int)subsweep_run_ctl_ints(g), ovf, flags,
-                       reset ? 1 : 0);
-    return hipGetLastError();
-}
-
-hipError_t launch_subsweep_run(const DevGeom& g, float* disk, const int16_t* n, const RunDesc& rd, uint32_t sweep,
-                               unsigned long long* stats, int* ovf, unsigned* ctl, uint32_t* flags, hipStream_t st,
-                               const LaunchTiming* tm) {
-    if (rd.nph < 1 || rd.nph > 4 || rd.ncz < 1 || (size_t)rd.nph * rd.ncz * (g.cps_y / 2) + kRunCtlHead >
-                                                         subsweep_run_ctl_ints(g))
-        return hipErrorInvalidValue;
-    const int64_t bytes = (int64_t)g.cps_x * g.cps_y * (g.nz_local + 2 * g.halo) * 3 * g.nmax * 4;
-    if (bytes >= ((int64_t)1 << 32) || g.nmax != 16) return hipErrorInvalidValue;   // 32-bit buffer offsets, nmax 16
-    // one wave per two-cell item of the XCD with the most planes, times 8: the round-robin dispatch
-    // gives every XCD blocks / 8 workgroups, each claims one item of its XCD's queue (the surplus ones
-    // exit at once); a dispatch that starves an XCD leaves items unclaimed: k_run_check flags it
-    const int64_t items_max = (int64_t)rd.nph * ((rd.ncz + 7) / 8) * (g.cps_y / 2) * ((g.cps_x / 2 + 1) / 2);
-    const unsigned blocks = (unsigned)(8 * items_max);
-    const size_t lds = sizeof(float) * (size_t)lds_floats_per_wave(kMainCap);
-    launch_k(k_subsweep_run<16, 16>, dim3(blocks), dim3(kWave), lds, st, tm, g, disk, n, rd, sweep, stats,
-             subsweep_capacity(g), ovf, ctl, flags);
-    return hipGetLastError();
-}
 
 hipError_t launch_colour_rows(const DevGeom& g, const float* src, float* dst, int colour, int mode, hipStream_t st) {
     int o[3];

@@ -1,4 +1,5 @@
-"""z-slab domain decomposition over ranks (one process per GPU), halo planes over RCCL.
+"""z-slab domain decomposition over ranks (one process per GPU); halo planes over the IPC transport
+(peer buffers mapped over xGMI, pulled by the library's copy kernels) or RCCL.
 
 The reference is single-GPU (start.cu:169-272); this is the build's multi-GPU path (SURVEY.md
 section 8e).  Rank r owns global cell planes z in [r*nz, (r+1)*nz) of a cps x cps x (world*nz)
@@ -16,9 +17,10 @@ The sweep plan (colour order, f, d) is a pure function of (seed, sweep) that eve
 itself, and the RNG counters use GLOBAL cell ids, so the result is bit-identical to the
 whole-box run for any number of ranks (tests/test_slab.py checks 2 ranks against 1).
 
-The engine and the transport are injected: the product path uses PmcContext (HIP) with torch
-device tensors and torch.distributed point-to-point (backend "nccl" = RCCL over xGMI); the CPU
-tests drive the same class with the C oracle and the gloo backend.
+Two drivers: SlabDriver, the product path (the C slab driver, pmc_slab_*; its schedule groups the
+phases into runs of equal z parity and exchanges once per run), and SlabSimulation, the legacy
+per-colour schedule above in Python over torch.distributed, whose engine and transport are injected
+so the CPU tests drive it with the C oracle and gloo.
 """
 from __future__ import annotations
 
@@ -94,7 +96,10 @@ def sends_for_self(sends, recvs):
 
 
 class SlabSimulation:
-    """Checkerboard sweeps on one z-slab with halo exchange after every phase and shift.
+    """LEGACY per-colour schedule (round 1), kept as the CPU-testable twin of the decomposition:
+    checkerboard sweeps on one z-slab with a halo exchange after every phase and shift, in Python over
+    torch.distributed (tests/test_slab.py drives it with the oracle and gloo).  The product multi-GPU
+    path is SlabDriver below (the C slab driver, pmc_slab_sweep).
 
     engine: object with phase(colour, sweep) and shift(sweep) acting on buffer `cur`, flipping
             `cur` in shift (PmcContext with attached state, or the test's oracle engine).
@@ -434,8 +439,11 @@ class SlabDriver:
     each way per run); after shiftCells only a z shift needs one more plane.  With halo=2 (two halo
     planes per side; PMC_SLAB_HALO=2 sets the default) the first run also visits the neighbour's
     boundary plane redundantly and a sweep needs ONE exchange, after shiftCells.
-    The host issues a sweep in a few dozen HIP/RCCL calls.  SlabSimulation above is the older per-colour schedule in Python
-    over torch.distributed; the CPU tests drive it with the oracle and gloo.
+    The host issues a sweep in a few dozen HIP calls.  Transports: IPC (default for world > 1: one
+    process per rank, the peers' buffers mapped, exchanges pulled by the library's copy kernels), RCCL,
+    local copies (one rank), or the in-process group (W ranks as threads of one process).
+    SlabSimulation above is the legacy per-colour schedule in Python over torch.distributed; the CPU
+    tests drive it with the oracle and gloo.
     """
 
     def __init__(self, cps: int, nz_local: int, rank: int, world: int, stream=None, atoms_per_rank: int = 0,

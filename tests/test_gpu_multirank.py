@@ -190,7 +190,7 @@ def test_local_group_missing_rank_fails_not_hangs(pmc):
 # deferred one is flushed by finish)
 _ROUND3 = {"PMC_SLAB_SPLIT_SHIFT": "0", "PMC_SLAB_DEFER_Z": "0"}   # round 3's schedule
 _BFULL = {"PMC_BOUNDARY_FULL": "1"}
-_RUNK = {"PMC_SLAB_RUNK": "1"}      # each run's interior planes as one dataflow launch
+_DIRECT = {"PMC_SLAB_DIRECT_HALO": "1"}   # one rank, no transport: boundary launches write the halo
 
 
 @pytest.mark.parametrize("chains,env,world,cps,nz,atoms", [
@@ -201,10 +201,8 @@ _RUNK = {"PMC_SLAB_RUNK": "1"}      # each run's interior planes as one dataflow
     (3, _ROUND3, 2, 32, 16, 120_000),
     (2, _BFULL, 4, 32, 8, 120_000),    # full-capacity boundary launches
     (2, _BFULL, 2, 16, 8, 10_000),
-    (1, _RUNK, 4, 32, 8, 120_000),     # 3 interior planes per run: XCDs 0-2 (one plane each)
-    (1, _RUNK, 2, 32, 16, 120_000),    # 7 per run
-    (1, _RUNK, 1, 32, 32, 120_000),    # one rank, 15 per run: two planes on XCDs 0-6
-    (1, _RUNK, 2, 48, 24, 400_000),    # 48^2 planes (24 colour cells per row: 12 waves), 11 per run
+    (2, _DIRECT, 1, 32, 32, 120_000),  # direct halo writes (one rank without a transport), z shifts
+    (2, {**_DIRECT, **_ROUND3}, 1, 16, 16, 10_000),
 ])
 def test_c_slab_driver_chain_count(pmc, oracle, chains, env, world, cps, nz, atoms):
     """PMC_SLAB_CHAINS=1 (one interior chain per rank: every phase one launch on the context
@@ -213,7 +211,8 @@ def test_c_slab_driver_chain_count(pmc, oracle, chains, env, world, cps, nz, ato
     stream, every other plane on the context stream without waiting for that exchange) and deferred
     z exchanges (a z shift's halo plane carried by the next sweep's first run exchange when that run
     does not read it), without both (PMC_SLAB_SPLIT_SHIFT=0, PMC_SLAB_DEFER_Z=0), and with
-    PMC_BOUNDARY_FULL=1 (boundary phases as one full-capacity launch),
+    PMC_BOUNDARY_FULL=1 (boundary phases as one full-capacity launch), and PMC_SLAB_DIRECT_HALO=1 (one
+    rank without a transport: the boundary launches write each row into the periodic halo too),
     through the in-process transport, equal the oracle's whole box over 8 sweeps with shifts along
     x, y and z both ways.  Subprocess: the switches are read once per process."""
     import subprocess
@@ -231,7 +230,10 @@ pmc_amd.lib()
 g = LocalGroup(world)
 keep = []
 def main(r):
-    d = SlabDriver(cps=cps, nz_local=nz, rank=r, world=world, atoms_total=atoms, local_group=g)
+    if world == 1:   # one rank without a transport: periodic halos by local copies (or direct writes)
+        d = SlabDriver(cps=cps, nz_local=nz, rank=0, world=1, atoms_total=atoms, transport="local")
+    else:
+        d = SlabDriver(cps=cps, nz_local=nz, rank=r, world=world, atoms_total=atoms, local_group=g)
     keep.append(d)
     lay = d.ctx.slab_layout()
     d.run(first, 8)

@@ -1,6 +1,11 @@
-"""Slab decomposition (multi-GPU path) on CPU: 2 gloo ranks driving the oracle through the same
-SlabSimulation class the RCCL product path uses; the result must equal the whole-box run
-bit for bit (global-id RNG counters, replicated sweep plan, halo exchange schedule)."""
+"""The LEGACY per-colour slab schedule on CPU: 2-4 gloo rank processes drive the oracle through
+SlabSimulation (pmc_amd/slab.py), the Python twin of round 1's schedule -- a halo exchange after every
+colour phase over torch.distributed.  It is not the product's schedule: the product multi-GPU path is
+the C slab driver (pmc_slab_sweep: runs of equal z parity, one exchange per run, deferred z planes),
+whose rank PROCESSES are tested on the GPU against the oracle through the IPC transport
+(tests/test_gpu_multiprocess.py) and whose schedule at world 1-8 through the in-process transport
+(tests/test_gpu_multirank.py).  What this file pins on CPU is the decomposition itself: global-id RNG
+counters, the replicated sweep plan and the halo shift rule reproduce the whole-box run bit for bit."""
 import socket
 
 import numpy as np
