@@ -15,6 +15,7 @@
 #                    default local), injected exchange delay us
 #   mp2bench         bench.py --gpus 2 --same-device --config 4 (rank processes, IPC)
 #   rocprof          rocprofv3 --kernel-trace --stats of the default bench command
+# A step may carry environment variables: PMC_QUAD_CELLS=40000@bench2 (A/B switches).
 set -o pipefail
 TAG=${1:?tag}; shift
 OUT=gpurun_out/$TAG
@@ -34,9 +35,18 @@ for ln in open(sys.argv[1]):
             p.get("state_bitwise_equal"), p.get("counters_equal")))
 EOF
 }
-for step in "$@"; do
-    log=$OUT/${step//[:\/]/_}.log
-    echo "== $step"
+for spec in "$@"; do
+    # VAR=VAL[,VAR=VAL...]@step runs the step with those environment variables (an A/B switch)
+    envs=()
+    step=$spec
+    if [[ $spec == *@* ]]; then
+        IFS=, read -ra envs <<< "${spec%%@*}"
+        step=${spec#*@}
+    fi
+    name=${spec//[:\/=,@ ]/_}
+    log=$OUT/$name.log
+    echo "== $spec"
+    for e in "${envs[@]}"; do export "$e"; done
     case $step in
         tests) timeout -k 10 900 $PYT tests -m gpu > $log 2>&1 ;;
         tests:*) timeout -k 10 600 $PYT tests -m gpu -k "${step#tests:}" > $log 2>&1 ;;
@@ -55,16 +65,15 @@ for step in "$@"; do
                 --no-cpu-baseline --steps 100 --warmup 20 > $log 2>&1 ;;
         mp2bench) timeout -k 10 400 python bench.py --gpus 2 --same-device --config 4 --steps 20 --warmup 5 \
                 --rank-timeout 360 > $log 2>&1 ;;
-        rocprof) (cd /tmp && export TMPDIR=/tmp) ; timeout -k 10 400 rocprofv3 --kernel-trace --stats \
+        rocprof) export TMPDIR=/tmp; timeout -k 10 400 rocprofv3 --kernel-trace --stats \
                 -d $OUT/rocprof -o bench -- python3 bench.py --steps 20 --warmup 5 > $log 2>&1 ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
     rc=$?
-    if [ $rc -ne 0 ]; then echo "step $step failed rc $rc"; tail -40 $log; exit $rc; fi
+    for e in "${envs[@]}"; do unset "${e%%=*}"; done
+    if [ $rc -ne 0 ]; then echo "step $spec failed rc $rc"; tail -40 $log; exit $rc; fi
     case $step in
-        tests*|mp) tail -1 $log ;;
-        smoke) tail -1 $log ;;
-        rocprof) grep '^{' $log > $OUT/${step}.json; summ $OUT/${step}.json ;;
-        *) grep '^{' $log > $OUT/${step//[:\/]/_}.json; summ $OUT/${step//[:\/]/_}.json ;;
+        tests*|mp|smoke) tail -1 $log ;;
+        *) grep '^{' $log > $OUT/$name.json; summ $OUT/$name.json ;;
     esac
 done
