@@ -11,8 +11,12 @@
  *   r    : float[3*N]             -- SoA positions x[N], y[N], z[N] (start.cu:186, :54-56)
  *   cell index = x + y*CPS + z*CPS^2  (get_cell_index, subsweep.h:14-16)
  *
- * Every entry point below cites the reference symbol it replaces.  Device pointers are HIP
- * device pointers in the reference layout.  All functions return PMC_OK (0) or a negative
+ * Every entry point below cites the reference symbol it replaces.  Device pointers a caller passes
+ * (pmc_subsweep, pmc_shift_cells, pmc_assign) and host arrays (pmc_copy_in/out, snapshots) are in
+ * the reference layout.  The context's OWN state (pmc_state, pmc_attach_state) is in the state
+ * layout pmc_state_layout reports: the reference rows, or x, y, z packed per slot (a cell's
+ * occupied slots one contiguous run); the entry points convert at the boundary.  A cell holds
+ * 3*nmax floats at cell*3*nmax in both.  All functions return PMC_OK (0) or a negative
  * pmc_status; they never print and never exit (the reference printf's and continues,
  * start.cu:213-216).  One host thread per context; all work is enqueued on the context's
  * stream (default: a stream created by pmc_create, or the one given to pmc_set_stream).
@@ -91,12 +95,18 @@ int pmc_set_stream(pmc_ctx* ctx, void* stream);
 /* The stream the context enqueues on (a hipStream_t), for ordering caller work against it. */
 int pmc_get_stream(pmc_ctx* ctx, void** stream);
 /* Use caller-owned device buffers as the context state instead of its own (e.g. torch
- * tensors for RCCL halo exchange).  Each disk buffer holds storage_cells*3*nmax floats, each
- * n buffer storage_cells int16; buffer 0 is the current state. */
+ * tensors for RCCL halo exchange).  Each disk buffer holds storage_cells*3*nmax floats in the
+ * state layout (pmc_state_layout), each n buffer storage_cells int16; buffer 0 is the current
+ * state. */
 int pmc_attach_state(pmc_ctx* ctx, float* disk0, int16_t* n0, float* disk1, int16_t* n1);
-/* Current state buffers (device pointers, reference layout), storage geometry. */
+/* Current state buffers (device pointers, state layout), storage geometry. */
 int pmc_state(pmc_ctx* ctx, float** disk, int16_t** n);
 int64_t pmc_storage_cells(const pmc_ctx* ctx);
+/* Layout of the state buffers: slot s of dimension d of a cell at float d*nmax + s
+ * (PMC_LAYOUT_REFERENCE, start.cu:188) or 3*s + d (PMC_LAYOUT_PACKED). */
+#define PMC_LAYOUT_REFERENCE 0
+#define PMC_LAYOUT_PACKED 1
+int pmc_state_layout(const pmc_ctx* ctx, int* layout);
 /* Last error message of this thread ("" if none). */
 const char* pmc_last_error(void);
 /* HIP devices visible to this process; PMC_ERR_NODEV (and *count = 0) when there is none.  Lets a
@@ -113,7 +123,9 @@ int pmc_init_r(pmc_ctx* ctx, int64_t n_atoms, float* d_r);
  * cell exceeds nmax, PMC_ERR_RANGE if a particle is outside the owned box. */
 int pmc_assign(pmc_ctx* ctx, const float* d_r, int64_t n_atoms, float* d_disk, int16_t* d_n);
 /* subsweep_kernel (subsweep.h:240-300): one checkerboard colour phase, offset = (ox,oy,oz)
- * in {0,1}^3 (start.cu:241-245).  `sweep` is the RNG counter (sweep index). */
+ * in {0,1}^3 (start.cu:241-245).  `sweep` is the RNG counter (sweep index).  d_disk: the reference
+ * layout (converted through a staging buffer when the state layout is packed), or one of the
+ * context's own state buffers. */
 int pmc_subsweep(pmc_ctx* ctx, float* d_disk, const int16_t* d_n, const int offset[3],
                  uint32_t sweep);
 /* shiftCells (shiftCells.h:28-144; semantics of the fixed copy

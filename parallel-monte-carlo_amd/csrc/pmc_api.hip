@@ -55,6 +55,9 @@ struct pmc_ctx {
     int32_t* tmp_idx = nullptr;
     float* d_r = nullptr;
     int64_t r_cap = 0;
+    // reference-layout staging for the ABI's caller buffers and host copies (PMC_AOS: the state is
+    // packed, the boundary converts; allocated on first use)
+    float* conv[2] = {nullptr, nullptr};
     hipStream_t stream = nullptr;
     bool own_stream = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -151,6 +154,14 @@ int64_t icbrt_ceil(int64_t n) {
 
 size_t disk_bytes(const pmc_ctx* c) { return sizeof(float) * 3 * (size_t)c->P.nmax * (size_t)c->cells; }
 size_t n_bytes(const pmc_ctx* c) { return sizeof(int16_t) * (size_t)c->cells; }
+
+// a caller's device buffer that is one of the context's own state buffers (state layout already)
+bool is_state_buffer(const pmc_ctx* c, const float* p) { return p == c->disk[0] || p == c->disk[1]; }
+
+// staging buffer k (storage-sized, reference layout <-> state layout conversions)
+hipError_t ensure_conv(pmc_ctx* c, int k) {
+    return c->conv[k] ? hipSuccess : hipMalloc(&c->conv[k], disk_bytes(c));
+}
 
 void free_state(pmc_ctx* c) {
     if (c->own_state) {
@@ -301,7 +312,7 @@ void pmc_destroy(pmc_ctx* c) {
     if (c->ovf_aux) (void)hipFree(c->ovf_aux);
     if (c->ovf_b) (void)hipFree(c->ovf_b);
     if (c->ovf_aux2) (void)hipFree(c->ovf_aux2);
-    for (void* m : {(void*)c->send_d, (void*)c->send_n, (void*)c->xflags})
+    for (void* m : {(void*)c->send_d, (void*)c->send_n, (void*)c->xflags, (void*)c->conv[0], (void*)c->conv[1]})
         if (m) (void)hipFree(m);
     if (c->tmp_cnt) (void)hipFree(c->tmp_cnt);
     if (c->tmp_idx) (void)hipFree(c->tmp_idx);
@@ -362,6 +373,12 @@ int pmc_state(pmc_ctx* c, float** disk, int16_t** n) {
 
 int64_t pmc_storage_cells(const pmc_ctx* c) { return c ? c->cells : -1; }
 
+int pmc_state_layout(const pmc_ctx* c, int* layout) {
+    if (!c || !layout) return fail(PMC_ERR_ARG, "null argument");
+    *layout = PMC_AOS ? PMC_LAYOUT_PACKED : PMC_LAYOUT_REFERENCE;
+    return PMC_OK;
+}
+
 int pmc_init_r(pmc_ctx* c, int64_t n_atoms, float* d_r) {
     if (!c || !d_r || n_atoms < 0) return fail(PMC_ERR_ARG, "bad argument");
     hipError_t e = launch_init_r(c->G, n_atoms, icbrt_ceil(n_atoms), d_r, c->stream);
@@ -375,7 +392,8 @@ int pmc_assign(pmc_ctx* c, const float* d_r, int64_t n_atoms, float* d_disk, int
         PMC_HIP(hipMalloc(&c->tmp_idx, sizeof(int32_t) * (size_t)c->cells * (size_t)c->P.nmax));
     }
     PMC_HIP(hipMemsetAsync(c->flags, 0, 16, c->stream));
-    hipError_t e = launch_assign(c->G, d_r, n_atoms, d_disk, d_n, c->tmp_cnt, c->tmp_idx, c->flags, c->stream);
+    hipError_t e = launch_assign(c->G, d_r, n_atoms, d_disk, d_n, c->tmp_cnt, c->tmp_idx, c->flags, c->stream, 0,
+                                 is_state_buffer(c, d_disk) ? 0 : 1);
     if (e != hipSuccess) return hip_fail(e, "assign launch");
     uint32_t fl = 0;
     PMC_HIP(hipMemcpyAsync(&fl, c->flags, 4, hipMemcpyDeviceToHost, c->stream));
@@ -392,9 +410,18 @@ int pmc_subsweep_range(pmc_ctx* c, float* d_disk, const int16_t* d_n, const int 
         if (offset[k] != 0 && offset[k] != 1) return fail(PMC_ERR_ARG, "offset must be in {0,1}^3");
     if (zl_begin < 0 || zl_end > c->P.nz_local || zl_begin > zl_end)
         return fail(PMC_ERR_ARG, "plane range outside the owned planes");
+    // a caller's reference-layout buffer runs through the staging buffer in the state layout
+    const bool conv = PMC_AOS && !is_state_buffer(c, d_disk);
+    float* run = d_disk;
+    if (conv) {
+        PMC_HIP(ensure_conv(c, 0));
+        PMC_HIP(launch_relayout(d_disk, c->conv[0], c->cells, c->P.nmax, 1, c->stream));
+        run = c->conv[0];
+    }
     LaunchTiming lt;
-    hipError_t e = launch_subsweep(c->G, d_disk, d_n, offset[0], offset[1], offset[2], sweep, c->stats, c->ovf,
+    hipError_t e = launch_subsweep(c->G, run, d_n, offset[0], offset[1], offset[2], sweep, c->stats, c->ovf,
                                    zl_begin, zl_end, c->stream, next_timing(c, 0, &lt));
+    if (e == hipSuccess && conv) e = launch_relayout(c->conv[0], d_disk, c->cells, c->P.nmax, 0, c->stream);
     return e == hipSuccess ? PMC_OK : hip_fail(e, "subsweep launch");
 }
 
@@ -408,8 +435,22 @@ int pmc_shift_cells(pmc_ctx* c, const float* din, const int16_t* nin, float* dou
     if (!c || !din || !nin || !dout || !nout) return fail(PMC_ERR_ARG, "null buffer");
     if (f < 0 || f > 2) return fail(PMC_ERR_ARG, "f must be 0, 1 or 2 (reference draws -1..1: start.cu:251)");
     if (din == dout || nin == nout) return fail(PMC_ERR_ARG, "shift is double-buffered: in != out");
+    // caller buffers in the reference layout run through the staging buffers in the state layout
+    const bool cin = PMC_AOS && !is_state_buffer(c, din), cout = PMC_AOS && !is_state_buffer(c, dout);
+    const float* rin = din;
+    float* rout = dout;
+    if (cin) {
+        PMC_HIP(ensure_conv(c, 0));
+        PMC_HIP(launch_relayout(din, c->conv[0], c->cells, c->P.nmax, 1, c->stream));
+        rin = c->conv[0];
+    }
+    if (cout) {
+        PMC_HIP(ensure_conv(c, 1));
+        rout = c->conv[1];
+    }
     LaunchTiming lt;
-    hipError_t e = launch_shift(c->G, din, nin, dout, nout, f, d, c->flags, c->stream, next_timing(c, 1, &lt));
+    hipError_t e = launch_shift(c->G, rin, nin, rout, nout, f, d, c->flags, c->stream, next_timing(c, 1, &lt));
+    if (e == hipSuccess && cout) e = launch_relayout(rout, dout, c->cells, c->P.nmax, 0, c->stream);
     return e == hipSuccess ? PMC_OK : hip_fail(e, "shift launch");
 }
 
@@ -736,7 +777,15 @@ int pmc_start(pmc_ctx* c, uint32_t first, int mc_passes, pmc_result* out) {
 int pmc_copy_out(pmc_ctx* c, float* h_disk, int16_t* h_n) {
     if (!c) return fail(PMC_ERR_ARG, "null ctx");
     if (int rj = slab_join(c)) return rj;
-    if (h_disk) PMC_HIP(hipMemcpyAsync(h_disk, c->disk[c->cur], disk_bytes(c), hipMemcpyDeviceToHost, c->stream));
+    if (h_disk) {   // the reference layout (PMC_AOS: converted on the device first)
+        const float* src = c->disk[c->cur];
+        if (PMC_AOS) {
+            PMC_HIP(ensure_conv(c, 0));
+            PMC_HIP(launch_relayout(src, c->conv[0], c->cells, c->P.nmax, 0, c->stream));
+            src = c->conv[0];
+        }
+        PMC_HIP(hipMemcpyAsync(h_disk, src, disk_bytes(c), hipMemcpyDeviceToHost, c->stream));
+    }
     if (h_n) PMC_HIP(hipMemcpyAsync(h_n, c->n[c->cur], n_bytes(c), hipMemcpyDeviceToHost, c->stream));
     PMC_HIP(hipStreamSynchronize(c->stream));
     return PMC_OK;
@@ -745,7 +794,15 @@ int pmc_copy_out(pmc_ctx* c, float* h_disk, int16_t* h_n) {
 int pmc_copy_in(pmc_ctx* c, const float* h_disk, const int16_t* h_n) {
     if (!c) return fail(PMC_ERR_ARG, "null ctx");
     if (int rj = slab_join(c)) return rj;
-    if (h_disk) PMC_HIP(hipMemcpyAsync(c->disk[c->cur], h_disk, disk_bytes(c), hipMemcpyHostToDevice, c->stream));
+    if (h_disk) {   // from the reference layout (PMC_AOS: converted on the device)
+        if (PMC_AOS) {
+            PMC_HIP(ensure_conv(c, 0));
+            PMC_HIP(hipMemcpyAsync(c->conv[0], h_disk, disk_bytes(c), hipMemcpyHostToDevice, c->stream));
+            PMC_HIP(launch_relayout(c->conv[0], c->disk[c->cur], c->cells, c->P.nmax, 1, c->stream));
+        } else {
+            PMC_HIP(hipMemcpyAsync(c->disk[c->cur], h_disk, disk_bytes(c), hipMemcpyHostToDevice, c->stream));
+        }
+    }
     if (h_n) PMC_HIP(hipMemcpyAsync(c->n[c->cur], h_n, n_bytes(c), hipMemcpyHostToDevice, c->stream));
     PMC_HIP(hipStreamSynchronize(c->stream));
     return PMC_OK;

@@ -39,6 +39,18 @@ constexpr int kStatCounters = 4;    // de_fixed, accepted, trials, evaluated
 __host__ __device__ constexpr int stat_index(int counter, int slot) {
     return PMC_STATS_LANES ? slot * kStatCounters + counter : counter * kStatSlots + slot;
 }
+// Cell layout of the context's state buffers (disk): cell c holds 3*nmax floats at c*3*nmax in both
+// layouts; slot s of dimension d sits at
+//   PMC_AOS = 0: d*nmax + s  -- the reference's rows x[nmax], y[nmax], z[nmax] (start.cu:188);
+//   PMC_AOS = 1: 3*s + d     -- x, y, z per slot: a cell's occupied slots are one contiguous run
+//                               (4.8 particles = 58 B: one 64-B line instead of parts of three rows).
+// The ABI's reference-layout buffers (pmc_copy_in/out, pmc_subsweep, pmc_shift_cells, pmc_assign)
+// are converted at the boundary (launch_relayout); the context's own state is always this layout.
+#ifndef PMC_AOS
+#define PMC_AOS 1
+#endif
+__host__ __device__ constexpr uint32_t lay_dim(int nm) { return PMC_AOS ? 1u : (uint32_t)nm; }   // between dimensions
+__host__ __device__ constexpr uint32_t lay_slot() { return PMC_AOS ? 3u : 1u; }                  // between slots
 constexpr int kSmallSweeps = 32;   // k_sweep_small: sweep plans per launch (pmc_run_small checks each launch)
 constexpr int kOvfHead = 2;        // ints of the subsweep overflow-queue header (pmc_kernels.hip)
 
@@ -118,8 +130,10 @@ hipError_t launch_shift_planes(const DevGeom& g, const float* din, const int16_t
                                int16_t* nout, int f, float d, uint32_t* flags, int zl_begin, int zl_end,
                                hipStream_t st, const LaunchTiming* tm);
 hipError_t launch_init_r(const DevGeom& g, int64_t n_atoms, int64_t n_cube, float* r, hipStream_t st);
+// ref_layout = 1: disk is a caller's buffer in the reference layout (pmc_assign); 0: the state layout
 hipError_t launch_assign(const DevGeom& g, const float* r, int64_t n_atoms, float* disk, int16_t* n,
-                         int32_t* tmp_cnt, int32_t* tmp_idx, uint32_t* flags, hipStream_t st, int clip = 0);
+                         int32_t* tmp_cnt, int32_t* tmp_idx, uint32_t* flags, hipStream_t st, int clip = 0,
+                         int ref_layout = 0);
 // segq: int[1 + energy_segments(g)] scratch, zeroed on st before the call
 size_t energy_segments(const DevGeom& g);
 hipError_t launch_energy(const DevGeom& g, const float* disk, const int16_t* n,
@@ -127,6 +141,9 @@ hipError_t launch_energy(const DevGeom& g, const float* disk, const int16_t* n,
 // the cells of one colour of one plane: mode 0 plane -> packed buffer, 1 packed -> plane,
 // 2 plane -> plane; (cps_x/2)*(cps_y/2)*3*nmax floats
 hipError_t launch_colour_rows(const DevGeom& g, const float* src, float* dst, int colour, int mode, hipStream_t st);
+// reference layout <-> the state layout (PMC_AOS) of `cells` cells: to_state = 1: ref -> state, 0: state ->
+// ref (src != dst; a no-op copy when the layouts agree)
+hipError_t launch_relayout(const float* src, float* dst, int64_t cells, int nmax, int to_state, hipStream_t st);
 // rehearsal only: a one-wave kernel that occupies `st` for `us` microseconds (injected exchange delay)
 hipError_t launch_spin(double us, hipStream_t st);
 // IPC halo transport (pmc_kernels.hip, pmc_slab_init_ipc): sequence flags and the pull copy

@@ -139,20 +139,49 @@ __device__ constexpr unsigned long long stage_lane_mask(int q) {
 
 // Loads from the disk buffer.  OFF32 (buffer < 4 GiB): 32-bit byte offsets -> global_load with an
 // SGPR base and a VGPR offset (no 64-bit address math per load); else 64-bit element addressing.
+// ld3 / st3: a slot's x, y, z (dstep = lay_dim: the floats between dimensions) from ONE pointer, so
+// the three accesses are provably adjacent (the packed layout: one dwordx3 access) or at immediate
+// offsets (the reference rows), instead of three 32-bit offsets the compiler cannot combine.
 template <int OFF32> struct DiskAddr;
 template <> struct DiskAddr<1> {
     static constexpr uint32_t kUnit = 4;   // offsets in bytes
-    __device__ static __forceinline__ float ld(const float* b, uint32_t off) {
-        return *(const float*)((const char*)b + (uint64_t)off);
+    __device__ static __forceinline__ const float* at(const float* b, uint32_t off) {
+        return (const float*)((const char*)b + (uint64_t)off);
     }
-    __device__ static __forceinline__ void st(float* b, uint32_t off, float v) {
-        *(float*)((char*)b + (uint64_t)off) = v;
+    __device__ static __forceinline__ float* at(float* b, uint32_t off) { return (float*)((char*)b + (uint64_t)off); }
+    __device__ static __forceinline__ float ld(const float* b, uint32_t off) { return *at(b, off); }
+    __device__ static __forceinline__ void st(float* b, uint32_t off, float v) { *at(b, off) = v; }
+    __device__ static __forceinline__ void ld3(const float* b, uint32_t off, uint32_t dstep, float& x, float& y,
+                                               float& z) {
+        const float* q = at(b, off);
+        x = q[0];
+        y = q[dstep];
+        z = q[2 * dstep];
+    }
+    __device__ static __forceinline__ void st3(float* b, uint32_t off, uint32_t dstep, float x, float y, float z) {
+        float* q = at(b, off);
+        q[0] = x;
+        q[dstep] = y;
+        q[2 * dstep] = z;
     }
 };
 template <> struct DiskAddr<0> {
     static constexpr uint32_t kUnit = 1;   // offsets in floats
     __device__ static __forceinline__ float ld(const float* b, uint32_t off) { return b[(uint64_t)off]; }
     __device__ static __forceinline__ void st(float* b, uint32_t off, float v) { b[(uint64_t)off] = v; }
+    __device__ static __forceinline__ void ld3(const float* b, uint32_t off, uint32_t dstep, float& x, float& y,
+                                               float& z) {
+        const float* q = b + (uint64_t)off;
+        x = q[0];
+        y = q[dstep];
+        z = q[2 * dstep];
+    }
+    __device__ static __forceinline__ void st3(float* b, uint32_t off, uint32_t dstep, float x, float y, float z) {
+        float* q = b + (uint64_t)off;
+        q[0] = x;
+        q[dstep] = y;
+        q[2 * dstep] = z;
+    }
 };
 
 // Philox4x32-10 with the host-computed key schedule (bit-identical to pmc_philox4x32_10: round
@@ -412,21 +441,18 @@ struct VisitLoads {
         const int p = lane & (HS - 1);
         const int kk = lane / HS;
         const int pp = p < nm ? p : 0;
-        const uint32_t pp_off = (uint32_t)pp * DiskAddr<OFF32>::kUnit;
-        const uint32_t nm_off = (uint32_t)nm * DiskAddr<OFF32>::kUnit;
+        const uint32_t pp_off = (uint32_t)pp * lay_slot() * DiskAddr<OFF32>::kUnit;
 #pragma unroll
         for (int q = 0; q < NP; ++q) {
             const int k = 1 + q * CPP + kk;
             const uint32_t off = (uint32_t)__shfl((int)k_off, hb + (k < 27 ? k : 26)) + pp_off;
-            vx[q] = DiskAddr<OFF32>::ld(disk, off);
-            vy[q] = DiskAddr<OFF32>::ld(disk, off + nm_off);
-            vz[q] = DiskAddr<OFF32>::ld(disk, off + 2 * nm_off);
+            DiskAddr<OFF32>::ld3(disk, off, lay_dim(nm), vx[q], vy[q], vz[q]);
         }
         const int l = lane < nm ? lane : 0;
         const float* own = disk + (uint64_t)cg.c * (uint32_t)(3 * nm);   // wave-uniform base
-        ownx = own[l];
-        owny = own[nm + l];
-        ownz = own[2 * nm + l];
+        ownx = own[(uint32_t)l * lay_slot()];
+        owny = own[lay_dim(nm) + (uint32_t)l * lay_slot()];
+        ownz = own[2u * lay_dim(nm) + (uint32_t)l * lay_slot()];
     }
 };
 
@@ -503,7 +529,6 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
     const bool edge = cg.edge;
     const int p = lane & (HS - 1);
     const int kk = lane / HS;
-    const uint32_t nm_off = (uint32_t)nm * DiskAddr<OFF32>::kUnit;
     const float (&vx)[NP] = ld.vx;
     const float (&vy)[NP] = ld.vy;
     const float (&vz)[NP] = ld.vz;
@@ -617,10 +642,10 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
                 }
                 const int cnt = __shfl(k_cnt, ks);
                 const int ps = HS + p;                                    // slot in the row
-                const uint32_t off = (uint32_t)__shfl((int)k_off, ks) + (uint32_t)(ps < nm ? ps : 0) * DiskAddr<OFF32>::kUnit;
-                float ux = DiskAddr<OFF32>::ld(disk, off);
-                float uy = DiskAddr<OFF32>::ld(disk, off + nm_off);
-                float uz = DiskAddr<OFF32>::ld(disk, off + 2 * nm_off);
+                const uint32_t off = (uint32_t)__shfl((int)k_off, ks) +
+                                     (uint32_t)(ps < nm ? ps : 0) * lay_slot() * DiskAddr<OFF32>::kUnit;
+                float ux, uy, uz;
+                DiskAddr<OFF32>::ld3(disk, off, lay_dim(nm), ux, uy, uz);
                 if constexpr (decltype(with_image)::value) {
                     ux = ux + __shfl(k_sx, ks);
                     uy = uy + __shfl(k_sy, ks);
@@ -866,17 +891,15 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
     // ---- 5. write back the own cell in shuffled order (cpy_D_sh_to_Disk, subsweep.h:29-36) ----
     if (lane < n_own) {
         using A = DiskAddr<OFF32>;
-        const uint32_t off = (c * (uint32_t)(3 * nm) + (uint32_t)lane) * A::kUnit;
-        A::st(disk, off, px_[lane]);
-        A::st(disk, off + (uint32_t)nm * A::kUnit, py_[lane]);
-        A::st(disk, off + 2u * (uint32_t)nm * A::kUnit, pz_[lane]);
+        const uint32_t off = (c * (uint32_t)(3 * nm) + (uint32_t)lane * lay_slot()) * A::kUnit;
+        A::st3(disk, off, lay_dim(nm), px_[lane], py_[lane], pz_[lane]);
         if constexpr (MIRROR) {
             const uint32_t r = mirror_mode == 0 ? (uint32_t)ta + (uint32_t)tb * (uint32_t)(g.cps_x >> 1)
                                                 : (uint32_t)x + (uint32_t)g.cps_x * (uint32_t)y;
-            float* m = mirror + (size_t)r * (3 * nm) + lane;
+            float* m = mirror + (size_t)r * (3 * nm) + (uint32_t)lane * lay_slot();
             m[0] = px_[lane];
-            m[nm] = py_[lane];
-            m[2 * nm] = pz_[lane];
+            m[lay_dim(nm)] = py_[lane];
+            m[2u * lay_dim(nm)] = pz_[lane];
         }
     }
     // fixed-point conversion only when something was accepted (pmc_to_fixed(0) == 0)
@@ -1296,8 +1319,8 @@ __device__ __forceinline__ void shift_cells_wave(const DevGeom& g, const float* 
     float own[3], nbv[3];
 #pragma unroll
     for (int dim = 0; dim < 3; ++dim) {
-        own[dim] = din[(uint64_t)c * (uint64_t)(3 * nm) + (uint64_t)(dim * nm + pp)];
-        nbv[dim] = din[(uint64_t)cnb * (uint64_t)(3 * nm) + (uint64_t)(dim * nm + pp)];
+        own[dim] = din[(uint64_t)c * (uint64_t)(3 * nm) + (uint64_t)(dim * lay_dim(nm) + pp * lay_slot())];
+        nbv[dim] = din[(uint64_t)cnb * (uint64_t)(3 * nm) + (uint64_t)(dim * lay_dim(nm) + pp * lay_slot())];
     }
     const int gsh = lane & ~(NSLOT - 1);
     const unsigned long long gmask = NSLOT == 64 ? ~0ull : ((1ull << (NSLOT & 63)) - 1ull);
@@ -1317,14 +1340,15 @@ __device__ __forceinline__ void shift_cells_wave(const DevGeom& g, const float* 
         const int dst = __popcll(km & below);
         if (dst < nm)
 #pragma unroll
-            for (int dim = 0; dim < 3; ++dim) dout[ob + (uint64_t)(dim * nm + dst)] = (dim == f) ? D + offset : own[dim];
+            for (int dim = 0; dim < 3; ++dim)
+                dout[ob + (uint64_t)(dim * lay_dim(nm) + dst * lay_slot())] = (dim == f) ? D + offset : own[dim];
     }
     if (take) {
         const int dst = nk + __popcll(tm & below);
         if (dst < nm)
 #pragma unroll
             for (int dim = 0; dim < 3; ++dim)
-                dout[ob + (uint64_t)(dim * nm + dst)] = (dim == f) ? ((Dn + offset) + s) : nbv[dim];
+                dout[ob + (uint64_t)(dim * lay_dim(nm) + dst * lay_slot())] = (dim == f) ? ((Dn + offset) + s) : nbv[dim];
     }
     if (live && p == 0) {
         nout[c] = (int16_t)(nnew > nm ? nm : nnew);
@@ -1485,20 +1509,17 @@ __global__ __launch_bounds__(kShiftThreads) void k_shift(DevGeom g, const float*
         cnbv[j] = cnb;
 #ifndef PMC_SHIFT_MASKED
         if constexpr (OFF32) {
-            const uint32_t oc = (c[j] * (uint32_t)(3 * nm) + (uint32_t)pp) * 4u;
-            const uint32_t on = (cnb * (uint32_t)(3 * nm) + (uint32_t)pp) * 4u;
-#pragma unroll
-            for (int dim = 0; dim < 3; ++dim) {
-                own[j][dim] = DiskAddr<1>::ld(din, oc + (uint32_t)(dim * nm) * 4u);
-                nbv[j][dim] = DiskAddr<1>::ld(din, on + (uint32_t)(dim * nm) * 4u);
-            }
+            const uint32_t oc = (c[j] * (uint32_t)(3 * nm) + (uint32_t)pp * lay_slot()) * 4u;
+            const uint32_t on = (cnb * (uint32_t)(3 * nm) + (uint32_t)pp * lay_slot()) * 4u;
+            DiskAddr<1>::ld3(din, oc, lay_dim(nm), own[j][0], own[j][1], own[j][2]);
+            DiskAddr<1>::ld3(din, on, lay_dim(nm), nbv[j][0], nbv[j][1], nbv[j][2]);
         } else {
-            const uint64_t oc = (uint64_t)c[j] * (uint64_t)(3 * nm) + (uint64_t)pp;
-            const uint64_t on = (uint64_t)cnb * (uint64_t)(3 * nm) + (uint64_t)pp;
+            const uint64_t oc = (uint64_t)c[j] * (uint64_t)(3 * nm) + (uint64_t)pp * lay_slot();
+            const uint64_t on = (uint64_t)cnb * (uint64_t)(3 * nm) + (uint64_t)pp * lay_slot();
 #pragma unroll
             for (int dim = 0; dim < 3; ++dim) {
-                own[j][dim] = din[oc + (uint64_t)(dim * nm)];
-                nbv[j][dim] = din[on + (uint64_t)(dim * nm)];
+                own[j][dim] = din[oc + (uint64_t)dim * lay_dim(nm)];
+                nbv[j][dim] = din[on + (uint64_t)dim * lay_dim(nm)];
             }
         }
 #endif
@@ -1507,12 +1528,12 @@ __global__ __launch_bounds__(kShiftThreads) void k_shift(DevGeom g, const float*
     // second round trip: only the occupied slots (partial rows: 32 B requests instead of lines)
 #pragma unroll
     for (int j = 0; j < U; ++j) {
-        const uint64_t oc = (uint64_t)c[j] * (uint64_t)(3 * nm) + (uint64_t)pp;
-        const uint64_t on = (uint64_t)cnbv[j] * (uint64_t)(3 * nm) + (uint64_t)pp;
+        const uint64_t oc = (uint64_t)c[j] * (uint64_t)(3 * nm) + (uint64_t)pp * lay_slot();
+        const uint64_t on = (uint64_t)cnbv[j] * (uint64_t)(3 * nm) + (uint64_t)pp * lay_slot();
 #pragma unroll
         for (int dim = 0; dim < 3; ++dim) {
-            own[j][dim] = p < ncur[j] ? din[oc + (uint64_t)(dim * nm)] : 0.0f;
-            nbv[j][dim] = p < nnb[j] ? din[on + (uint64_t)(dim * nm)] : 0.0f;
+            own[j][dim] = p < ncur[j] ? din[oc + (uint64_t)dim * lay_dim(nm)] : 0.0f;
+            nbv[j][dim] = p < nnb[j] ? din[on + (uint64_t)dim * lay_dim(nm)] : 0.0f;
         }
     }
 #endif
@@ -1528,27 +1549,30 @@ __global__ __launch_bounds__(kShiftThreads) void k_shift(DevGeom g, const float*
         const unsigned long long tm = (__ballot(take) >> gsh) & gmask;
         const int nk = __popcll(km);
         const int nnew = nk + __popcll(tm);
-        // output slot `dst` of dimension row `dim` of cell c[j]: element offset c*3nm + dim*nm + dst
-        auto out_at = [&](int dim, int dst) -> float* {
+        // output slot `dst` of cell c[j] (element offset c*3nm + dst*lay_slot; dimension dim at +dim*lay_dim)
+        auto out_at = [&](int dst) -> float* {
+            const uint32_t e = (uint32_t)dst * lay_slot();
             if constexpr (OFF32)
-                return (float*)((char*)dout + (uint64_t)((c[j] * (uint32_t)(3 * nm) + (uint32_t)(dim * nm + dst)) * 4u));
+                return (float*)((char*)dout + (uint64_t)((c[j] * (uint32_t)(3 * nm) + e) * 4u));
             else
-                return dout + (uint64_t)c[j] * (uint64_t)(3 * nm) + (uint64_t)(dim * nm + dst);
+                return dout + (uint64_t)c[j] * (uint64_t)(3 * nm) + (uint64_t)e;
         };
         if (keep) {
             const int dst = __popcll(km & below);
             if (dst < nm) {
+                float* q = out_at(dst);
 #pragma unroll
                 for (int dim = 0; dim < 3; ++dim)
-                    shift_store(out_at(dim, dst), (dim == f) ? D + offset[j] : own[j][dim]);
+                    shift_store(q + dim * lay_dim(nm), (dim == f) ? D + offset[j] : own[j][dim]);
             }
         }
         if (take) {
             const int dst = nk + __popcll(tm & below);
             if (dst < nm) {
+                float* q = out_at(dst);
 #pragma unroll
-                for (int dim = 0; dim < 3; ++dim)
-                    shift_store(out_at(dim, dst), (dim == f) ? ((Dn + offset[j]) + s) : nbv[j][dim]);   // own offset (VS shiftCells.h:96)
+                for (int dim = 0; dim < 3; ++dim)   // own offset (VS shiftCells.h:96)
+                    shift_store(q + dim * lay_dim(nm), (dim == f) ? ((Dn + offset[j]) + s) : nbv[j][dim]);
             }
         }
         if (live[j] && p == 0) {
@@ -1623,7 +1647,7 @@ __global__ void k_assign_count(DevGeom g, const float* __restrict__ r, int64_t n
 // then write the cell's rows.
 __global__ void k_assign_fill(DevGeom g, const float* __restrict__ r, int64_t n_atoms,
                               const int32_t* __restrict__ tmp_cnt, const int32_t* __restrict__ tmp_idx,
-                              float* __restrict__ disk, int16_t* __restrict__ n, int64_t cells) {
+                              float* __restrict__ disk, int16_t* __restrict__ n, int64_t cells, int ref_layout) {
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= cells) return;
     const int nm = g.nmax;
@@ -1638,9 +1662,11 @@ __global__ void k_assign_fill(DevGeom g, const float* __restrict__ r, int64_t n_
     }
     for (int k = 0; k < cnt; ++k) {
         const int64_t i = ids[k];
-        disk[c * 3 * nm + k] = r[i];
-        disk[c * 3 * nm + nm + k] = r[i + n_atoms];
-        disk[c * 3 * nm + 2 * nm + k] = r[i + 2 * n_atoms];
+        // (the reference layout for a caller's buffer, the state layout for the context's own)
+        const int64_t ds = ref_layout ? nm : (int64_t)lay_dim(nm), ss = ref_layout ? 1 : (int64_t)lay_slot();
+        disk[c * 3 * nm + k * ss] = r[i];
+        disk[c * 3 * nm + ds + k * ss] = r[i + n_atoms];
+        disk[c * 3 * nm + 2 * ds + k * ss] = r[i + 2 * n_atoms];
     }
     n[c] = (int16_t)cnt;
 }
@@ -1885,10 +1911,8 @@ __global__ __launch_bounds__(kWave) void k_energy(DevGeom g, const float* __rest
                 vact[q] = e < ncells && p < c_cnt;
                 if (vact[q]) {
                     using DA = DiskAddr<OFF32>;
-                    const uint32_t off = ((uint32_t)c_idx * (uint32_t)(3 * nm) + (uint32_t)p) * DA::kUnit;
-                    vx[q] = DA::ld(disk, off);
-                    vy[q] = DA::ld(disk, off + (uint32_t)nm * DA::kUnit);
-                    vz[q] = DA::ld(disk, off + 2u * (uint32_t)nm * DA::kUnit);
+                    const uint32_t off = ((uint32_t)c_idx * (uint32_t)(3 * nm) + (uint32_t)p * lay_slot()) * DA::kUnit;
+                    DA::ld3(disk, off, lay_dim(nm), vx[q], vy[q], vz[q]);
                 }
                 if (edge) {   // periodic images (a +0 add changes no difference: interior cells skip it)
                     // (cross-lane reads outside the branch: an inactive source lane supplies nothing)
@@ -1943,10 +1967,11 @@ __global__ __launch_bounds__(kWave) void k_energy(DevGeom g, const float* __rest
                     float ux = 0.0f, uy = 0.0f, uz = 0.0f;
                     if (act) {
                         using DA = DiskAddr<OFF32>;
-                        const uint32_t off = ((uint32_t)c_idx * (uint32_t)(3 * nm) + (uint32_t)ps) * DA::kUnit;
-                        ux = DA::ld(disk, off) + isx;
-                        uy = DA::ld(disk, off + (uint32_t)nm * DA::kUnit) + isy;
-                        uz = DA::ld(disk, off + 2u * (uint32_t)nm * DA::kUnit) + isz;
+                        const uint32_t off = ((uint32_t)c_idx * (uint32_t)(3 * nm) + (uint32_t)ps * lay_slot()) * DA::kUnit;
+                        DA::ld3(disk, off, lay_dim(nm), ux, uy, uz);
+                        ux = ux + isx;
+                        uy = uy + isy;
+                        uz = uz + isz;
                     }
                     put(act && (!filter || near(ux, uy, uz)), ux, uy, uz);
                 }
@@ -2183,16 +2208,13 @@ __global__ __launch_bounds__(kWave) void k_energy_rows(DevGeom g, const float* _
     constexpr int CPP = kWave / HS;
     using DA = DiskAddr<OFF32>;
     const int p = lane % HS, ce = lane / HS;
-    const uint32_t nmu = (uint32_t)nm * DA::kUnit;
     for (int e0 = 0; e0 < E; e0 += CPP) {
         const int e = e0 + ce;
         const int2 rc = rec[e < E ? e : E];
         const int c_n = rc.y >> 16, c_s = rc.y & 0xffff;
         if (e < E && p < c_n) {
-            const uint32_t off = ((uint32_t)rc.x * (uint32_t)(3 * nm) + (uint32_t)p) * DA::kUnit;
-            ex_[c_s + p] = DA::ld(disk, off);
-            ey_[c_s + p] = DA::ld(disk, off + nmu);
-            ez_[c_s + p] = DA::ld(disk, off + 2u * nmu);
+            const uint32_t off = ((uint32_t)rc.x * (uint32_t)(3 * nm) + (uint32_t)p * lay_slot()) * DA::kUnit;
+            DA::ld3(disk, off, lay_dim(nm), ex_[c_s + p], ey_[c_s + p], ez_[c_s + p]);
         }
     }
     if constexpr (HS < NSLOT) {
@@ -2208,10 +2230,8 @@ __global__ __launch_bounds__(kWave) void k_energy_rows(DevGeom g, const float* _
             const int c_n = rc.y >> 16, c_s = rc.y & 0xffff;
             for (int ps = HS + p; ps < NSLOT; ps += HS) {
                 if (ce < nc && ps < c_n) {
-                    const uint32_t off = ((uint32_t)rc.x * (uint32_t)(3 * nm) + (uint32_t)ps) * DA::kUnit;
-                    ex_[c_s + ps] = DA::ld(disk, off);
-                    ey_[c_s + ps] = DA::ld(disk, off + nmu);
-                    ez_[c_s + ps] = DA::ld(disk, off + 2u * nmu);
+                    const uint32_t off = ((uint32_t)rc.x * (uint32_t)(3 * nm) + (uint32_t)ps * lay_slot()) * DA::kUnit;
+                    DA::ld3(disk, off, lay_dim(nm), ex_[c_s + ps], ey_[c_s + ps], ez_[c_s + ps]);
                 }
             }
         }
@@ -2349,6 +2369,22 @@ __global__ void k_selftest(const uint32_t* __restrict__ words, int count, float*
     out_d[2 * i + 1] = (double)pmc_to_fixed((double)out_f[4 * i + 3]);
 }
 
+// Reference layout <-> state layout (pmc_internal.h, PMC_AOS): element e of cell c, e = d*nmax + s in
+// the reference, d + 3*s in the packed layout.  One thread per float, coalesced on the destination.
+__global__ void k_relayout(const float* __restrict__ src, float* __restrict__ dst, int64_t total, int nm,
+                           int to_state) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int64_t row = 3 * (int64_t)nm;
+    const int64_t c = i / row;
+    const int e = (int)(i - c * row);
+    int d, sl;                                      // (dimension, slot) of destination element e
+    if (to_state) { d = (int)(e % 3); sl = e / 3; }  // destination packed, source reference
+    else { d = e / nm; sl = e - d * nm; }            // destination reference, source packed
+    const int es = to_state ? d * nm + sl : 3 * sl + d;
+    dst[i] = src[c * row + es];
+}
+
 // Strong-scaling rehearsal only (PMC_XFER_DELAY_US): one wave that keeps the exchange stream busy
 // for `ticks` of the 100 MHz real-time counter after a halo exchange -- the xGMI transfer time and
 // RCCL latency a one-GPU rehearsal does not see.  Bounded by the tick count (no memory access).
@@ -2358,6 +2394,15 @@ __global__ void k_spin(uint64_t ticks) {
 }
 
 }  // namespace
+
+hipError_t launch_relayout(const float* src, float* dst, int64_t cells, int nmax, int to_state, hipStream_t st) {
+    const int64_t total = cells * 3 * (int64_t)nmax;
+    if (total <= 0) return hipSuccess;
+    if (!PMC_AOS) return hipMemcpyAsync(dst, src, sizeof(float) * (size_t)total, hipMemcpyDeviceToDevice, st);
+    hipLaunchKernelGGL(k_relayout, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, src, dst, total, nmax,
+                       to_state);
+    return hipGetLastError();
+}
 
 hipError_t launch_spin(double us, hipStream_t st) {
     const uint64_t ticks = us > 0.0 ? (uint64_t)(us * 100.0) : 0;   // s_memrealtime: 100 MHz
@@ -2824,7 +2869,8 @@ hipError_t launch_init_r(const DevGeom& g, int64_t n_atoms, int64_t n_cube, floa
 }
 
 hipError_t launch_assign(const DevGeom& g, const float* r, int64_t n_atoms, float* disk, int16_t* n,
-                         int32_t* tmp_cnt, int32_t* tmp_idx, uint32_t* flags, hipStream_t st, int clip) {
+                         int32_t* tmp_cnt, int32_t* tmp_idx, uint32_t* flags, hipStream_t st, int clip,
+                         int ref_layout) {
     const int64_t cells = (int64_t)g.cps_x * g.cps_y * (g.nz_local + 2 * g.halo);
     hipError_t e = hipMemsetAsync(tmp_cnt, 0, sizeof(int32_t) * (size_t)cells, st);
     if (e != hipSuccess) return e;
@@ -2833,7 +2879,8 @@ hipError_t launch_assign(const DevGeom& g, const float* r, int64_t n_atoms, floa
         hipLaunchKernelGGL(k_assign_count, grid, block, 0, st, g, r, n_atoms, tmp_cnt, tmp_idx, flags, clip);
     }
     dim3 grid2((unsigned)((cells + 255) / 256)), block2(256);
-    hipLaunchKernelGGL(k_assign_fill, grid2, block2, 0, st, g, r, n_atoms, tmp_cnt, tmp_idx, disk, n, cells);
+    hipLaunchKernelGGL(k_assign_fill, grid2, block2, 0, st, g, r, n_atoms, tmp_cnt, tmp_idx, disk, n, cells,
+                       ref_layout);
     return hipGetLastError();
 }
 

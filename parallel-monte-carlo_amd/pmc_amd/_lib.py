@@ -48,6 +48,7 @@ class Result(C.Structure):
 PMC_FLAG_FULL_SHUFFLE = 1
 PMC_OK, PMC_ERR_ARG, PMC_ERR_HIP, PMC_ERR_OVERFLOW, PMC_ERR_RANGE, PMC_ERR_NODEV = 0, -1, -2, -3, -4, -5
 PMC_IPC_HANDLE_BYTES = 1024     # include/pmc.h
+PMC_LAYOUT_REFERENCE, PMC_LAYOUT_PACKED = 0, 1
 
 
 class PmcError(RuntimeError):
@@ -100,6 +101,7 @@ def lib():
         _sig(L, "pmc_attach_state", i32, _vp, _vp, _vp, _vp, _vp)
         _sig(L, "pmc_state", i32, _vp, C.POINTER(_vp), C.POINTER(_vp))
         _sig(L, "pmc_storage_cells", i64, _vp)
+        _sig(L, "pmc_state_layout", i32, _vp, C.POINTER(C.c_int))
         _sig(L, "pmc_init_r", i32, _vp, i64, _vp)
         _sig(L, "pmc_assign", i32, _vp, _vp, i64, _vp, _vp)
         _sig(L, "pmc_subsweep", i32, _vp, _vp, _vp, C.POINTER(C.c_int * 3), u32)

@@ -113,6 +113,13 @@ class PmcContext:
     def attach_state(self, disk0, n0, disk1, n1):
         check("pmc_attach_state", lib().pmc_attach_state(self._h, _ptr(disk0), _ptr(n0), _ptr(disk1), _ptr(n1)))
 
+    def state_layout(self) -> int:
+        """Layout of the state buffers (pmc_state_layout): 0 the reference rows (slot s of dimension d
+        at d*nmax + s), 1 packed (3*s + d).  Host copies and snapshots are always the reference layout."""
+        v = C.c_int(0)
+        check("pmc_state_layout", lib().pmc_state_layout(self._h, C.byref(v)))
+        return v.value
+
     def state_ptrs(self):
         d, n = C.c_void_p(), C.c_void_p()
         check("pmc_state", lib().pmc_state(self._h, C.byref(d), C.byref(n)))

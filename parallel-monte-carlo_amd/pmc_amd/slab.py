@@ -389,8 +389,12 @@ class SlabSimulation:
 
     # ---- views ------------------------------------------------------------------------
     def owned(self):
-        """(disk, n) of the owned planes of the current buffer."""
-        return self.disk[self.cur][1:-1], self.n[self.cur][1:-1]
+        """(disk, n) of the owned planes of the current buffer; disk as (..., 3, nmax) in the reference
+        order whatever the state layout (a packed state is viewed transposed)."""
+        d = self.disk[self.cur][1:-1]
+        if getattr(self.engine, "state_layout", None) and self.engine.state_layout() == 1:
+            d = d.reshape(*d.shape[:-2], d.shape[-1], d.shape[-2]).transpose(-1, -2)
+        return d, self.n[self.cur][1:-1]
 
 
 def _all_gather_bytes(data: bytes, world: int, group=None) -> list:
