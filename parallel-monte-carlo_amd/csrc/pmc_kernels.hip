@@ -1485,6 +1485,24 @@ __global__ __launch_bounds__(kShiftThreads) void k_shift(DevGeom g, const float*
     uint32_t c[U], cnbv[U];
     int ncur[U], nnb[U];
     float offset[U], offset_nb[U], own[U][3], nbv[U][3];
+    // slot pp of cell c[j] and of its dir-neighbour (x, y, z: one dwordx3 each in the packed layout)
+    auto load_slots = [&](int j) {
+        if constexpr (OFF32) {
+            const uint32_t oc = (c[j] * (uint32_t)(3 * nm) + (uint32_t)pp * lay_slot()) * 4u;
+            const uint32_t on = (cnbv[j] * (uint32_t)(3 * nm) + (uint32_t)pp * lay_slot()) * 4u;
+            DiskAddr<1>::ld3(din, oc, lay_dim(nm), own[j][0], own[j][1], own[j][2]);
+            DiskAddr<1>::ld3(din, on, lay_dim(nm), nbv[j][0], nbv[j][1], nbv[j][2]);
+        } else {
+            const uint64_t oc = (uint64_t)c[j] * (uint64_t)(3 * nm) + (uint64_t)pp * lay_slot();
+            const uint64_t on = (uint64_t)cnbv[j] * (uint64_t)(3 * nm) + (uint64_t)pp * lay_slot();
+            own[j][0] = din[oc];
+            own[j][1] = din[oc + lay_dim(nm)];
+            own[j][2] = din[oc + 2 * lay_dim(nm)];
+            nbv[j][0] = din[on];
+            nbv[j][1] = din[on + lay_dim(nm)];
+            nbv[j][2] = din[on + 2 * lay_dim(nm)];
+        }
+    };
 #pragma unroll
     for (int j = 0; j < U; ++j) {
         const int x = (bx * U + j) * CPB + (int)(threadIdx.x / NSLOT);
@@ -1507,36 +1525,12 @@ __global__ __launch_bounds__(kShiftThreads) void k_shift(DevGeom g, const float*
         ncur[j] = live[j] ? nc0 : 0;
         nnb[j] = live[j] ? nn0 : 0;
         cnbv[j] = cnb;
-#ifndef PMC_SHIFT_MASKED
-        if constexpr (OFF32) {
-            const uint32_t oc = (c[j] * (uint32_t)(3 * nm) + (uint32_t)pp * lay_slot()) * 4u;
-            const uint32_t on = (cnb * (uint32_t)(3 * nm) + (uint32_t)pp * lay_slot()) * 4u;
-            DiskAddr<1>::ld3(din, oc, lay_dim(nm), own[j][0], own[j][1], own[j][2]);
-            DiskAddr<1>::ld3(din, on, lay_dim(nm), nbv[j][0], nbv[j][1], nbv[j][2]);
-        } else {
-            const uint64_t oc = (uint64_t)c[j] * (uint64_t)(3 * nm) + (uint64_t)pp * lay_slot();
-            const uint64_t on = (uint64_t)cnb * (uint64_t)(3 * nm) + (uint64_t)pp * lay_slot();
-#pragma unroll
-            for (int dim = 0; dim < 3; ++dim) {
-                own[j][dim] = din[oc + (uint64_t)dim * lay_dim(nm)];
-                nbv[j][dim] = din[on + (uint64_t)dim * lay_dim(nm)];
-            }
-        }
-#endif
+        // every slot of both cells in the same round trip as the counts.  (Loading only slots [0, 8)
+        // here and the rest after the counts when a cell of the wave holds more -- two of the packed
+        // cell's three 64-B lines -- measured slower: 0.169 against 0.144 ms,
+        // profiles/r05i_shift_half_ab.txt; so did loading only the occupied slots, r05h.)
+        load_slots(j);
     }
-#ifdef PMC_SHIFT_MASKED
-    // second round trip: only the occupied slots (partial rows: 32 B requests instead of lines)
-#pragma unroll
-    for (int j = 0; j < U; ++j) {
-        const uint64_t oc = (uint64_t)c[j] * (uint64_t)(3 * nm) + (uint64_t)pp * lay_slot();
-        const uint64_t on = (uint64_t)cnbv[j] * (uint64_t)(3 * nm) + (uint64_t)pp * lay_slot();
-#pragma unroll
-        for (int dim = 0; dim < 3; ++dim) {
-            own[j][dim] = p < ncur[j] ? din[oc + (uint64_t)dim * lay_dim(nm)] : 0.0f;
-            nbv[j][dim] = p < nnb[j] ? din[on + (uint64_t)dim * lay_dim(nm)] : 0.0f;
-        }
-    }
-#endif
 #pragma unroll
     for (int j = 0; j < U; ++j) {
         const float xf = f == 0 ? own[j][0] : (f == 1 ? own[j][1] : own[j][2]);
@@ -2840,11 +2834,11 @@ hipError_t launch_shift_planes(const DevGeom& g, const float* din, const int16_t
     const dim3 block(kShiftThreads);
 #endif
     const int z0 = zl_begin;
-    // PMC_SHIFT_OFF32=1: 32-bit byte offsets when the storage is below 4 GiB (103 VGPRs, 4 waves per
-    // SIMD, -10% VALU) -- measured no faster (0.203-0.204 against 0.199-0.203 ms,
-    // profiles/r04q_shift_off32_ab.txt): the launch is bound by its DRAM bursts, not by issue or
-    // occupancy, so the 64-bit form stays the default
-    static const bool off32_env = env_cells("PMC_SHIFT_OFF32", 0) != 0;
+    // 32-bit byte offsets when the storage is below 4 GiB (PMC_SHIFT_OFF32=0: the 64-bit form).  With
+    // the reference rows it measured no faster (0.203-0.204 against 0.199-0.203 ms,
+    // profiles/r04q_shift_off32_ab.txt); with the packed layout 0.146-0.147 against 0.151-0.153 ms
+    // (profiles/r05h_shift_variants_ab.txt), so it is the default now
+    static const bool off32_env = env_cells("PMC_SHIFT_OFF32", 1) != 0;
     const int64_t bytes = (int64_t)g.cps_x * g.cps_y * (g.nz_local + 2 * g.halo) * 3 * g.nmax * 4;
     const bool off32 = off32_env && bytes < ((int64_t)1 << 32);
     auto go = [&](auto ns) {
