@@ -2409,21 +2409,17 @@ hipError_t launch_spin(double us, hipStream_t st) {
 // IPC halo transport (pmc_slab_init_ipc): the slab driver's point-to-point messages between rank
 // processes of one node (or several processes on one GPU), through IPC-mapped peer buffers and
 // per-rank sequence flags in uncached device memory -- no host round trip per exchange.  Exchange k
-// on the exchange stream is two launches:
-//   k_xfer_flag: ready[me] = k (every earlier kernel of the stream has ended: its writes are
-//     released); then wait until ready[p] >= k for each peer p this rank receives from, and until
-//     pulled[p] >= k' for each peer that read this rank's buffers in the previous exchange k' (so
-//     this exchange's copies and everything after it may overwrite them);
-//   k_xfer: pull every message from the peer's buffer into ours, grid-wide; the last block to
-//     finish stores pulled[me] = k.
-// The copy is its own launch, after the wait kernel has completed: the kernel-start acquire the
-// command processor performs then orders its reads after the peers' kernel-end releases, exactly as
-// a cross-stream event wait would; no shader-side cache maintenance on the peer's data is relied on
-// (the AMDGPU memory model's acquire invalidates only non-local L2 lines, and what an IPC mapping of
-// a same-device peer's buffer counts as is not specified).  k_xfer_flag alone (no signal) settles the last
-// exchange's "pulled" before host-visible points (pmc_slab_finish, copies, teardown).  Waits give up
-// after `timeout` ticks of the 100 MHz real-time counter and set error-flag bit 9 (value 512)
-// instead of hanging the GPU.
+// on the exchange stream is ONE launch, k_xfer<true>: block 0 publishes ready[me] = k (every
+// earlier kernel of the stream has ended: its writes are released); every block waits until
+// ready[p] >= k for each peer p this rank receives from, and until pulled[p] >= k' for each peer
+// that read this rank's buffers in the previous exchange k' (so this exchange and everything after
+// it may overwrite them); then pulls its share of every message from the peer's buffer into ours;
+// the last block to finish stores pulled[me] = k.  PMC_IPC_FUSED=0 splits it into k_xfer_flag (the
+// signal and the waits) and k_xfer<false> (the copy), whose reads then follow the command
+// processor's kernel-start acquire rather than the shader's.  k_xfer_flag alone (no signal) settles
+// the last exchange's "pulled" before host-visible points (pmc_slab_finish, copies, teardown).
+// Waits give up after `timeout` ticks of the 100 MHz real-time counter and set error-flag bit 9
+// (value 512) instead of hanging the GPU.
 // ------------------------------------------------------------------------------------------
 namespace {
 
@@ -2475,7 +2471,23 @@ __device__ __forceinline__ void xfer_units(const XferSeg& s, int shift) {
     for (; i < n; i += stride) dst[i] = src[i];
 }
 
-__global__ void __launch_bounds__(256) k_xfer(XferCopy cp, uint64_t* pulled, uint64_t seq, unsigned* done) {
+// WAIT (the one-launch form, PMC_IPC_FUSED): block 0 publishes ready[me] = seq and every block's
+// thread 0 waits for w itself (system-scope acquire loads: the fence after the satisfied load
+// invalidates the CU's L1 and the XCD's non-coherent L2 lines -- the peer's buffer as seen through
+// its mapping: NC for another GPU's memory; this GPU's own memory is kept coherent across the XCDs'
+// L2s by the cache probes of the PTE C-bit, AMDGPU memory model, gfx942 family) before the block's
+// threads read past the workgroup barrier.  Grid <= 64 blocks: waiting blocks hold wave slots, and
+// several rank processes may share one GPU.
+template <bool WAIT>
+__global__ void __launch_bounds__(256) k_xfer(XferCopy cp, uint64_t* pulled, uint64_t seq, unsigned* done,
+                                               XferFlags w, uint64_t* ready, uint64_t timeout, uint32_t* err) {
+    if constexpr (WAIT) {
+        if (threadIdx.x == 0) {
+            if (blockIdx.x == 0) flag_store(ready, seq);
+            (void)flags_wait(w, timeout, err);
+        }
+        __syncthreads();
+    }
     for (int k = 0; k < cp.n; ++k) {
         const XferSeg& s = cp.seg[k];
         switch (s.shift) {
@@ -2517,10 +2529,23 @@ hipError_t launch_xfer(const XferCopy& cp, const XferFlags& w, uint64_t* ready, 
             return hipErrorInvalidValue;
         units += (s.bytes + 15) / 16;
     }
-    hipLaunchKernelGGL(k_xfer_flag, dim3(1), dim3(kWave), 0, st, ready, seq, w, timeout_ticks, err);
+    // PMC_IPC_FUSED=0: the wait as a launch of its own before the copy (the copy's reads then follow
+    // the command processor's kernel-start acquire instead of the shader's)
+    static const bool fused = [] {
+        const char* v = std::getenv("PMC_IPC_FUSED");
+        return !(v && std::atoi(v) == 0);
+    }();
     const uint64_t want = (units + 1023) / 1024;
-    const unsigned blocks = (unsigned)(want < 1 ? 1 : want > 256 ? 256 : want);
-    hipLaunchKernelGGL(k_xfer, dim3(blocks), dim3(256), 0, st, cp, pulled, seq, done);
+    if (fused) {
+        const unsigned blocks = (unsigned)(want < 1 ? 1 : want > 64 ? 64 : want);
+        hipLaunchKernelGGL(k_xfer<true>, dim3(blocks), dim3(256), 0, st, cp, pulled, seq, done, w, ready, timeout_ticks,
+                           err);
+    } else {
+        hipLaunchKernelGGL(k_xfer_flag, dim3(1), dim3(kWave), 0, st, ready, seq, w, timeout_ticks, err);
+        const unsigned blocks = (unsigned)(want < 1 ? 1 : want > 256 ? 256 : want);
+        hipLaunchKernelGGL(k_xfer<false>, dim3(blocks), dim3(256), 0, st, cp, pulled, seq, done, w, ready,
+                           timeout_ticks, err);
+    }
     return hipGetLastError();
 }
 

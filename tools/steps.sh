@@ -11,6 +11,7 @@
 #   bench            default bench line (config 3, the driver's --steps 20 --warmup 5)
 #   bench2           config 2
 #   slab1            config 3 through the slab driver, one rank, local halos
+#   bench5           config 5 rehearsal (one 256x256x32 slab, halos through a one-rank RCCL communicator)
 #   emu<R>[-<tp>][-d<us>]   config-4 rehearsal of R ranks (one rank's slab), transport tp (local|ipc|rccl,
 #                    default local), injected exchange delay us
 #   mp2bench         bench.py --gpus 2 --same-device --config 4 (rank processes, IPC)
@@ -55,6 +56,7 @@ for spec in "$@"; do
         bench) timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $log 2>&1 ;;
         bench2) timeout -k 10 300 python bench.py --config 2 --steps 160 --warmup 8 > $log 2>&1 ;;
         slab1) timeout -k 10 300 python bench.py --slab --no-cpu-baseline --steps 20 --warmup 5 > $log 2>&1 ;;
+        bench5) timeout -k 10 300 python bench.py --config 5 --no-cpu-baseline --steps 20 --warmup 5 > $log 2>&1 ;;
         emu*)
             spec=${step#emu}; R=${spec%%-*}; tp=local; dl=0
             IFS=- read -ra parts <<< "$spec"
