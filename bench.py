@@ -543,19 +543,13 @@ def main() -> int:
     if not slab:
         sim = pmc_amd.PmcContext(cps, stream=stream.cuda_stream)
         sim.init_lattice(atoms)
-        from pmc_amd.plan import sweep_plan
-        plans = {}
 
         if config == "2":
             def one_sweep(s):       # config 2's step: ONE colour phase, colour s % 8 at sweep s // 8
                 sim.phase(s % 8, s // 8)
         else:
-            def one_sweep(s):
-                if s not in plans:
-                    plans[s] = sweep_plan(1234, s, 2.5)
-                for colour in plans[s][0]:
-                    sim.phase(colour, s)
-                sim.shift(s)
+            def one_sweep(s):   # pmc_sweep: 8 colour phases (in plane chains) + shiftCells, all in C
+                sim.sweep(s)
 
         def finish():
             pass
@@ -615,8 +609,18 @@ def main() -> int:
     elif not slab:
         n_owned = n_h.astype(np.int64)
         stencil = stencil_counts(n_owned, (cps, cps, cps))
-        sub_launch_bytes = staged_bytes(n_owned, stencil) / 8.0
-        roof_kernel = "k_subsweep<16,16,true> (one colour phase of the whole box)"
+        phase_bytes = staged_bytes(n_owned, stencil) / 8.0
+        # pmc_sweep's plane chains (pmc_sweep_layout): each colour phase is one launch per chain, the
+        # chains' launches concurrent; the roofline is per PHASE (its span: earliest launch start to
+        # latest stop, HIP events on the dispatch packets), launch_ms the per-launch mean
+        sweep_chains = sim.sweep_layout()
+        per_chain = [staged_bytes(n_owned[a * plane:b * plane], stencil[a * plane:b * plane]) / 8.0
+                     for a, b in sweep_chains]
+        sub_launch_bytes = sum(per_chain) / len(per_chain)
+        roof_kernel = ("k_subsweep<16,16,true> (one colour phase of the whole box" +
+                       (f" as {len(sweep_chains)} concurrent launches, plane chains " +
+                        " and ".join(f"[{a},{b})" for a, b in sweep_chains) +
+                        "; achieved/frac per phase over its span" if len(sweep_chains) > 1 else "") + ")")
     else:
         n_owned = n_h[plane * drv.halo:plane * (nz_local + drv.halo)].astype(np.int64)
         stencil = slab_stencil_counts(n_h, cps, nz_local, drv.halo)
@@ -663,6 +667,7 @@ def main() -> int:
     elapsed = time.perf_counter() - t0
     st = sim.stats()
     tm = sim.timing_kinds(False)
+    span_ms, span_n = sim.phase_spans() if (not slab and config == "3") else (0.0, 0)
     trials_local = st["trials"]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
@@ -693,6 +698,9 @@ def main() -> int:
         n_launch = tm["n_subsweep"]
         avg_launch_s = (tm["subsweep_ms"] / n_launch * 1e-3) if n_launch else None
         achieved = (sub_launch_bytes / avg_launch_s / 1e9) if avg_launch_s else None
+        phase_s = (span_ms / span_n * 1e-3) if span_n else None
+        if phase_s:   # chained whole-box phases: bytes of a phase over the phase's span
+            achieved = phase_bytes / phase_s / 1e9
         traffic = traffic_from_profile(config, slab, nz_local)
         # FP32 work of the moves (14 FLOP per pair evaluation, old + new position,
         # against the S_c - 1 stencil partners of each evaluated move; the mean stencil of the
@@ -701,11 +709,12 @@ def main() -> int:
         if avg_launch_s and not slab:
             ne = n_owned > 0
             s_mean = float(stencil[ne].mean()) if ne.any() else 0.0
-            launches = args.steps * (1 if config == "2" else 8)
-            flop = 28.0 * st["evaluated"] / launches * max(s_mean - 1.0, 0.0)
-            fp32 = {"achieved": flop / avg_launch_s / 1e12, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": flop / avg_launch_s / 1e12 / FP32_PEAK_TFLOPS, "flop_per_launch": flop,
-                    "model": "28 FLOP x (mean stencil - 1) per evaluated move (SURVEY.md 8d)"}
+            phases = args.steps * (1 if config == "2" else 8)
+            flop = 28.0 * st["evaluated"] / phases * max(s_mean - 1.0, 0.0)     # per colour phase
+            t_ph = phase_s or avg_launch_s
+            fp32 = {"achieved": flop / t_ph / 1e12, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": flop / t_ph / 1e12 / FP32_PEAK_TFLOPS, "flop_per_phase": flop,
+                    "model": "28 FLOP x (mean stencil - 1) per evaluated move (SURVEY.md 8d), per colour phase"}
         valu = valu_from_profile() if config == "3" else None   # profiled on the config-3 launch
         shift_bytes = None
         if tm["n_shift"]:
@@ -720,6 +729,8 @@ def main() -> int:
                 "kernel": roof_kernel,
                 "launch_ms": avg_launch_s * 1e3 if avg_launch_s else None,
                 "launches_timed": n_launch,
+                **({"phase_ms": phase_s * 1e3, "phases_timed": span_n,
+                    "algorithmic_bytes_per_phase": phase_bytes} if phase_s else {}),
                 "shift_ms": tm["shift_ms"] / tm["n_shift"] if tm["n_shift"] else None,
                 "shift": ({"algorithmic_bytes_per_launch": shift_bytes,
                            "achieved": shift_bytes / (tm["shift_ms"] / tm["n_shift"] * 1e-3) / 1e9,

@@ -263,6 +263,15 @@ int pmc_slab_observables(pmc_ctx* ctx, int with_energy, pmc_stats* out, double* 
  * pmc_phase_range_on launches (other streams: they overlap [0], durations do not add). */
 int pmc_timing(pmc_ctx* ctx, int enable, double* subsweep_ms, int* n_subsweep, double* shift_ms, int* n_shift);
 int pmc_timing_kinds(pmc_ctx* ctx, int enable, double ms[3], int count[3]);
+/* Colour phases that pmc_sweep splits over plane chains (pmc_sweep_layout) run as concurrent
+ * launches: the last pmc_timing / pmc_timing_kinds call also summed each such phase's span, from its
+ * earliest launch start to its latest stop; this returns that sum and the number of phases. */
+int pmc_timing_phase_spans(pmc_ctx* ctx, double* span_ms, int* n_phases);
+/* pmc_sweep's plane chains (whole box): *n_chains (1 or 2; PMC_SWEEP_CHAINS=1 forces one), chain j over
+ * local planes [borders[j], borders[j+1]).  Two chains: each colour phase is two launches on two
+ * streams; the halves' launch tails overlap (the runs of equal z parity make them independent; the
+ * slab driver's rule, pmc_slab_sweep). */
+int pmc_sweep_layout(pmc_ctx* ctx, int* n_chains, int borders[3]);
 /* Pause (paused = 1) or resume the per-launch events of pmc_timing without collecting them (no
  * synchronization): a caller times a sample of its launches, e.g. every k-th sweep, and the events'
  * own cost (about 1.3% of a sweep when every launch carries them) shrinks with the sample. */

@@ -58,6 +58,11 @@ struct pmc_ctx {
     // reference-layout staging for the ABI's caller buffers and host copies (PMC_AOS: the state is
     // packed, the boundary converts; allocated on first use)
     float* conv[2] = {nullptr, nullptr};
+    // whole-box sweeps in two plane chains (enqueue_sweep): the second chain's stream, the chains'
+    // "previous run" events [chain][parity], and the context stream's "sweep start" event
+    hipStream_t hs = nullptr;
+    hipEvent_t ev_c[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+    hipEvent_t ev_s = nullptr;
     hipStream_t stream = nullptr;
     bool own_stream = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -67,6 +72,10 @@ struct pmc_ctx {
     bool timing_paused = false;           // pmc_timing_pause: events off without collecting
     std::vector<hipEvent_t> tev;
     std::vector<int> tkind;                // 0 subsweep (interior / context stream), 1 shift, 2 subsweep (boundary / caller stream)
+    std::vector<int64_t> tphase;           // colour phase of a timed launch split over plane chains (-1: none)
+    int64_t phase_seq = 0;                 // next phase id (enqueue_sweep_chains)
+    double span_ms = 0.0;                  // pmc_timing_kinds: summed spans of those phases (pmc_timing_phase_spans)
+    int span_n = 0;
     uint32_t graph_first = 0;
     int graph_count = 0;
     int graph_cur = -1;
@@ -188,7 +197,7 @@ int slab_pending_zdir(const pmc_ctx* c);     // a deferred z-shift halo exchange
 
 // the next timing slot when pmc_timing is on (nullptr otherwise): events ride on the launch's
 // dispatch packet (hipExtLaunchKernelGGL), no extra packets in the stream
-const LaunchTiming* next_timing(pmc_ctx* c, int kind, LaunchTiming* lt) {
+const LaunchTiming* next_timing(pmc_ctx* c, int kind, LaunchTiming* lt, int64_t phase = -1) {
     if (!c->timing || c->timing_paused) return nullptr;
     const size_t k = c->tkind.size();
     while (c->tev.size() < 2 * (k + 1)) {
@@ -197,13 +206,80 @@ const LaunchTiming* next_timing(pmc_ctx* c, int kind, LaunchTiming* lt) {
         c->tev.push_back(e);
     }
     c->tkind.push_back(kind);
+    c->tphase.push_back(phase);
     lt->start = c->tev[2 * k];
     lt->stop = c->tev[2 * k + 1];
     return lt;
 }
 
-int enqueue_sweep(pmc_ctx* c, uint32_t sweep) {
+// Whole-box sweep in TWO plane chains (PMC_SWEEP_CHAINS, default 2): the planes [0, zs) on the context
+// stream and [zs, nz) on a second stream, zs = 2*(nz/4).  As in the slab driver (pmc_slab_sweep), the
+// 8 phases form runs of equal z parity q; in a run only parity-q planes change, each reading its
+// own plane and the parity 1-q planes next to it, which no phase of the run writes -- so the two
+// halves' launch chains are independent for a whole run, and each half's launch tails overlap the
+// other's work.  At a run boundary each chain waits for the other's previous run (the planes next to
+// its borders, the periodic one included: plane 0 and plane nz-1 are neighbours).  shiftCells joins
+// both chains on the context stream; the second stream starts each sweep after it.  Cells of a colour
+// are independent, so any split of a phase gives the same result bit for bit.
+int chain_count(const pmc_ctx* c) {
+    static const int env = [] {
+        const char* v = std::getenv("PMC_SWEEP_CHAINS");
+        return v ? std::atoi(v) : 2;
+    }();
+    return env == 2 && c->P.nz_local >= 8 ? 2 : 1;
+}
+
+int enqueue_sweep_chains(pmc_ctx* c, uint32_t sweep, const pmc_sweep_plan_t& plan) {
+    if (!c->hs) {
+        PMC_HIP(hipStreamCreateWithFlags(&c->hs, hipStreamNonBlocking));
+        for (auto& r : c->ev_c)
+            for (auto& e : r) PMC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        PMC_HIP(hipEventCreateWithFlags(&c->ev_s, hipEventDisableTiming));
+    }
+    if (!c->ovf_aux) {   // the second chain's overflow queue
+        PMC_HIP(hipMalloc(&c->ovf_aux, c->ovf_bytes));
+        PMC_HIP(hipMemsetAsync(c->ovf_aux, 0, c->ovf_bytes, c->stream));
+    }
+    const int nz = c->P.nz_local, zs = 2 * (nz / 4);
+    hipStream_t st[2] = {c->stream, c->hs};
+    int* ovf[2] = {c->ovf, c->ovf_aux};
+    // the second stream after everything issued on the context stream so far (the previous shift)
+    PMC_HIP(hipEventRecord(c->ev_s, c->stream));
+    PMC_HIP(hipStreamWaitEvent(c->hs, c->ev_s, 0));
+    int k = 0;
+    while (k < 8) {
+        const int q = plan.order[k] % 2;
+        int k1 = k;
+        while (k1 < 8 && plan.order[k1] % 2 == q) ++k1;
+        for (int j = 0; j < 2; ++j) {
+            if (k > 0) PMC_HIP(hipStreamWaitEvent(st[j], c->ev_c[1 - j][1 - q], 0));   // the other's previous run
+            for (int kk = k; kk < k1; ++kk) {
+                int o[3];
+                pmc_colour_offset(plan.order[kk], o);
+                LaunchTiming lt;
+                hipError_t e = launch_subsweep(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep, c->stats,
+                                               ovf[j], j == 0 ? 0 : zs, j == 0 ? zs : nz, st[j],
+                                               next_timing(c, 0, &lt, c->phase_seq + kk));
+                if (e != hipSuccess) return hip_fail(e, "subsweep launch");
+            }
+            PMC_HIP(hipEventRecord(c->ev_c[j][q], st[j]));
+        }
+        k = k1;
+    }
+    c->phase_seq += 8;
+    PMC_HIP(hipEventRecord(c->ev_s, c->hs));
+    PMC_HIP(hipStreamWaitEvent(c->stream, c->ev_s, 0));   // shiftCells reads every plane
+    LaunchTiming lt;
+    hipError_t e = launch_shift(c->G, c->disk[c->cur], c->n[c->cur], c->disk[c->cur ^ 1], c->n[c->cur ^ 1],
+                                plan.f, plan.d, c->flags, c->stream, next_timing(c, 1, &lt));
+    if (e != hipSuccess) return hip_fail(e, "shift launch");
+    c->cur ^= 1;
+    return PMC_OK;
+}
+
+int enqueue_sweep(pmc_ctx* c, uint32_t sweep, bool chains = true) {
     const pmc_sweep_plan_t plan = pmc_plan_for_sweep_ex(c->P.seed, sweep, c->P.w, c->P.flags);
+    if (chains && !c->P.halo && chain_count(c) == 2) return enqueue_sweep_chains(c, sweep, plan);
     for (int k = 0; k < 8; ++k) {
         int o[3];
         pmc_colour_offset(plan.order[k], o);
@@ -318,6 +394,12 @@ void pmc_destroy(pmc_ctx* c) {
     if (c->tmp_idx) (void)hipFree(c->tmp_idx);
     if (c->d_r) (void)hipFree(c->d_r);
     for (hipEvent_t e : c->tev) (void)hipEventDestroy(e);
+    if (c->hs) {
+        (void)hipStreamSynchronize(c->hs);
+        (void)hipStreamDestroy(c->hs);
+    }
+    for (hipEvent_t e : {c->ev_c[0][0], c->ev_c[0][1], c->ev_c[1][0], c->ev_c[1][1], c->ev_s})
+        if (e) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
@@ -599,7 +681,7 @@ int pmc_run_graph(pmc_ctx* c, uint32_t first, int count) {
         c->timing = false;
         PMC_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
         int rc = PMC_OK;
-        for (int k = 0; k < count && rc == PMC_OK; ++k) rc = enqueue_sweep(c, first + (uint32_t)k);
+        for (int k = 0; k < count && rc == PMC_OK; ++k) rc = enqueue_sweep(c, first + (uint32_t)k, false);
         hipError_t e = hipStreamEndCapture(c->stream, &graph);
         c->cur = cur0;
         c->timing = timing;
@@ -2338,11 +2420,33 @@ int pmc_timing_kinds(pmc_ctx* c, int enable, double ms[3], int count[3]) {
         if (c->slab)
             for (hipStream_t h : c->slab->hi)
                 if (h) PMC_HIP(hipStreamSynchronize(h));
+        if (c->hs) PMC_HIP(hipStreamSynchronize(c->hs));
         for (size_t k = 0; k < c->tkind.size(); ++k) {
             float t = 0.0f;
             PMC_HIP(hipEventElapsedTime(&t, c->tev[2 * k], c->tev[2 * k + 1]));
             a[c->tkind[k]] += t;
             ++na[c->tkind[k]];
+        }
+        // a colour phase split over plane chains: its launches run concurrently, its duration is the
+        // span from the earliest start to the latest stop (times relative to the first start event)
+        c->span_ms = 0.0;
+        c->span_n = 0;
+        for (size_t k = 0; k < c->tkind.size(); ++k) {
+            if (c->tphase[k] < 0) continue;
+            bool first = true;
+            for (size_t j = 0; j < k; ++j) first = first && c->tphase[j] != c->tphase[k];
+            if (!first) continue;
+            float lo = 1e30f, hi = -1e30f;
+            for (size_t j = k; j < c->tkind.size(); ++j) {
+                if (c->tphase[j] != c->tphase[k]) continue;
+                float t0 = 0.0f, t1 = 0.0f;
+                PMC_HIP(hipEventElapsedTime(&t0, c->tev[0], c->tev[2 * j]));
+                PMC_HIP(hipEventElapsedTime(&t1, c->tev[0], c->tev[2 * j + 1]));
+                lo = t0 < lo ? t0 : lo;
+                hi = t1 > hi ? t1 : hi;
+            }
+            c->span_ms += hi - lo;
+            ++c->span_n;
         }
     }
     for (int k = 0; k < 3; ++k) {
@@ -2350,8 +2454,26 @@ int pmc_timing_kinds(pmc_ctx* c, int enable, double ms[3], int count[3]) {
         if (count) count[k] = na[k];
     }
     c->tkind.clear();
+    c->tphase.clear();
     c->timing = enable != 0;
     c->timing_paused = false;
+    return PMC_OK;
+}
+
+int pmc_timing_phase_spans(pmc_ctx* c, double* span_ms, int* n_phases) {
+    if (!c || !span_ms || !n_phases) return fail(PMC_ERR_ARG, "null argument");
+    *span_ms = c->span_ms;
+    *n_phases = c->span_n;
+    return PMC_OK;
+}
+
+int pmc_sweep_layout(pmc_ctx* c, int* n_chains, int borders[3]) {
+    if (!c || !n_chains || !borders) return fail(PMC_ERR_ARG, "null argument");
+    const int nz = c->P.nz_local;
+    *n_chains = (!c->P.halo && chain_count(c) == 2) ? 2 : 1;
+    borders[0] = 0;
+    borders[1] = *n_chains == 2 ? 2 * (nz / 4) : nz;
+    borders[2] = nz;
     return PMC_OK;
 }
 

@@ -240,6 +240,20 @@ class PmcContext:
         return {"subsweep_ms": ms[0], "n_subsweep": cnt[0], "shift_ms": ms[1], "n_shift": cnt[1],
                 "boundary_ms": ms[2], "n_boundary": cnt[2]}
 
+    def phase_spans(self) -> tuple:
+        """(summed span ms, phases) of the colour phases pmc_sweep split over plane chains, from the last
+        timing()/timing_kinds() call (pmc_timing_phase_spans)."""
+        ms, n = C.c_double(0.0), C.c_int(0)
+        check("pmc_timing_phase_spans", lib().pmc_timing_phase_spans(self._h, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+    def sweep_layout(self) -> list:
+        """pmc_sweep's plane chains as (first plane, end plane) pairs (pmc_sweep_layout)."""
+        n = C.c_int(0)
+        b = (C.c_int * 3)()
+        check("pmc_sweep_layout", lib().pmc_sweep_layout(self._h, C.byref(n), C.byref(b)))
+        return [(b[j], b[j + 1]) for j in range(n.value)]
+
     def timing_pause(self, paused: bool) -> None:
         """Per-launch events off (paused) or back on without collecting them (pmc_timing_pause)."""
         check("pmc_timing_pause", lib().pmc_timing_pause(self._h, int(paused)))

@@ -28,9 +28,10 @@ import json, sys
 for ln in open(sys.argv[1]):
     if ln.startswith("{"):
         d = json.loads(ln); r = d.get("roofline") or {}; p = d.get("parity") or {}
-        print("%s value %.4g ms/step %.4f launch %s shift %s frac %s parity %s/%s" % (
+        print("%s value %.4g ms/step %.4f launch %s phase %s shift %s frac %s parity %s/%s" % (
             sys.argv[1].split("/")[-1], d["value"], d["ms_per_step"],
             "%.4f" % r["launch_ms"] if r.get("launch_ms") else None,
+            "%.4f" % r["phase_ms"] if r.get("phase_ms") else None,
             "%.4f" % r["shift_ms"] if r.get("shift_ms") else None,
             "%.4f" % r["frac"] if r.get("frac") else None,
             p.get("state_bitwise_equal"), p.get("counters_equal")))
