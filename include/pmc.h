@@ -267,11 +267,13 @@ int pmc_timing_kinds(pmc_ctx* ctx, int enable, double ms[3], int count[3]);
  * launches: the last pmc_timing / pmc_timing_kinds call also summed each such phase's span, from its
  * earliest launch start to its latest stop; this returns that sum and the number of phases. */
 int pmc_timing_phase_spans(pmc_ctx* ctx, double* span_ms, int* n_phases);
-/* pmc_sweep's plane chains (whole box): *n_chains (1 or 2; PMC_SWEEP_CHAINS=1 forces one), chain j over
- * local planes [borders[j], borders[j+1]).  Two chains: each colour phase is two launches on two
- * streams; the halves' launch tails overlap (the runs of equal z parity make them independent; the
+/* pmc_sweep's plane chains (whole box): *n_chains (1, 2 or 4: PMC_SWEEP_CHAINS, default 2; fewer when
+ * the box has under 4 planes per chain), chain j over local planes [borders[j], borders[j+1]) (entries
+ * past n_chains: nz).  More than one chain: each colour phase is one launch per chain, on streams of
+ * their own; the chains' launch tails overlap (the runs of equal z parity make them independent; the
  * slab driver's rule, pmc_slab_sweep). */
-int pmc_sweep_layout(pmc_ctx* ctx, int* n_chains, int borders[3]);
+#define PMC_SWEEP_MAX_CHAINS 4
+int pmc_sweep_layout(pmc_ctx* ctx, int* n_chains, int borders[PMC_SWEEP_MAX_CHAINS + 1]);
 /* Pause (paused = 1) or resume the per-launch events of pmc_timing without collecting them (no
  * synchronization): a caller times a sample of its launches, e.g. every k-th sweep, and the events'
  * own cost (about 1.3% of a sweep when every launch carries them) shrinks with the sample. */

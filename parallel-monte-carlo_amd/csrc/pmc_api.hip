@@ -58,10 +58,12 @@ struct pmc_ctx {
     // reference-layout staging for the ABI's caller buffers and host copies (PMC_AOS: the state is
     // packed, the boundary converts; allocated on first use)
     float* conv[2] = {nullptr, nullptr};
-    // whole-box sweeps in two plane chains (enqueue_sweep): the second chain's stream, the chains'
-    // "previous run" events [chain][parity], and the context stream's "sweep start" event
-    hipStream_t hs = nullptr;
-    hipEvent_t ev_c[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+    // whole-box sweeps in plane chains (enqueue_sweep): chains 1.. streams and overflow queues (chain 0:
+    // the context stream and ovf), the chains' "previous run" events [chain][parity], and the context
+    // stream's "sweep start" event
+    hipStream_t hs[PMC_SWEEP_MAX_CHAINS - 1] = {};
+    int* ovf_ch[PMC_SWEEP_MAX_CHAINS - 1] = {};
+    hipEvent_t ev_c[PMC_SWEEP_MAX_CHAINS][2] = {};
     hipEvent_t ev_s = nullptr;
     hipStream_t stream = nullptr;
     bool own_stream = false;
@@ -212,53 +214,70 @@ const LaunchTiming* next_timing(pmc_ctx* c, int kind, LaunchTiming* lt, int64_t 
     return lt;
 }
 
-// Whole-box sweep in TWO plane chains (PMC_SWEEP_CHAINS, default 2): the planes [0, zs) on the context
-// stream and [zs, nz) on a second stream, zs = 2*(nz/4).  As in the slab driver (pmc_slab_sweep), the
-// 8 phases form runs of equal z parity q; in a run only parity-q planes change, each reading its
-// own plane and the parity 1-q planes next to it, which no phase of the run writes -- so the two
-// halves' launch chains are independent for a whole run, and each half's launch tails overlap the
-// other's work.  At a run boundary each chain waits for the other's previous run (the planes next to
-// its borders, the periodic one included: plane 0 and plane nz-1 are neighbours).  shiftCells joins
-// both chains on the context stream; the second stream starts each sweep after it.  Cells of a colour
-// are independent, so any split of a phase gives the same result bit for bit.
+// Whole-box sweep in plane chains (PMC_SWEEP_CHAINS = 1, 2 (default) or 4): chain j runs the planes
+// [b_j, b_{j+1}), b_j = 2*((j*nz)/(2*chains)) (even borders), chain 0 on the context stream, the others
+// on streams of their own.  As in the slab driver (pmc_slab_sweep), the 8 phases form runs of equal z
+// parity q; in a run only parity-q planes change, each reading its own plane and the parity 1-q planes
+// next to it, which no phase of the run writes -- so the chains are independent for a whole run, and
+// each chain's launch tails overlap the others' work.  At a run boundary each chain waits for its two
+// neighbours' previous runs (the planes next to its borders, the periodic one included: plane 0 and
+// plane nz-1 are neighbours).  shiftCells joins the chains on the context stream; the other streams
+// start each sweep after it.  Cells of a colour are independent, so any split of a phase gives the
+// same result bit for bit.
 int chain_count(const pmc_ctx* c) {
     static const int env = [] {
         const char* v = std::getenv("PMC_SWEEP_CHAINS");
         return v ? std::atoi(v) : 2;
     }();
-    return env == 2 && c->P.nz_local >= 8 ? 2 : 1;
+    if (c->P.halo) return 1;
+    for (int n = env >= PMC_SWEEP_MAX_CHAINS ? PMC_SWEEP_MAX_CHAINS : env; n > 1; n /= 2)
+        if (c->P.nz_local >= 4 * n) return n;   // chains of >= 4 planes
+    return 1;
 }
+int chain_border(int nz, int n, int j) { return 2 * ((j * nz) / (2 * n)); }
 
-int enqueue_sweep_chains(pmc_ctx* c, uint32_t sweep, const pmc_sweep_plan_t& plan) {
-    if (!c->hs) {
-        PMC_HIP(hipStreamCreateWithFlags(&c->hs, hipStreamNonBlocking));
+int enqueue_sweep_chains(pmc_ctx* c, uint32_t sweep, const pmc_sweep_plan_t& plan, int n) {
+    if (!c->ev_s) {
         for (auto& r : c->ev_c)
             for (auto& e : r) PMC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         PMC_HIP(hipEventCreateWithFlags(&c->ev_s, hipEventDisableTiming));
     }
-    if (!c->ovf_aux) {   // the second chain's overflow queue
-        PMC_HIP(hipMalloc(&c->ovf_aux, c->ovf_bytes));
-        PMC_HIP(hipMemsetAsync(c->ovf_aux, 0, c->ovf_bytes, c->stream));
+    for (int j = 1; j < n; ++j) {
+        if (!c->hs[j - 1]) PMC_HIP(hipStreamCreateWithFlags(&c->hs[j - 1], hipStreamNonBlocking));
+        if (!c->ovf_ch[j - 1]) {   // chain j's overflow queue
+            PMC_HIP(hipMalloc(&c->ovf_ch[j - 1], c->ovf_bytes));
+            PMC_HIP(hipMemsetAsync(c->ovf_ch[j - 1], 0, c->ovf_bytes, c->stream));
+        }
     }
-    const int nz = c->P.nz_local, zs = 2 * (nz / 4);
-    hipStream_t st[2] = {c->stream, c->hs};
-    int* ovf[2] = {c->ovf, c->ovf_aux};
-    // the second stream after everything issued on the context stream so far (the previous shift)
+    const int nz = c->P.nz_local;
+    hipStream_t st[PMC_SWEEP_MAX_CHAINS];
+    int* ovf[PMC_SWEEP_MAX_CHAINS];
+    st[0] = c->stream;
+    ovf[0] = c->ovf;
+    for (int j = 1; j < n; ++j) {
+        st[j] = c->hs[j - 1];
+        ovf[j] = c->ovf_ch[j - 1];
+    }
+    // the other streams after everything issued on the context stream so far (the previous shift)
     PMC_HIP(hipEventRecord(c->ev_s, c->stream));
-    PMC_HIP(hipStreamWaitEvent(c->hs, c->ev_s, 0));
-    int k = 0;
+    for (int j = 1; j < n; ++j) PMC_HIP(hipStreamWaitEvent(st[j], c->ev_s, 0));
+    int k = 0, q = 0;
     while (k < 8) {
-        const int q = plan.order[k] % 2;
+        q = plan.order[k] % 2;
         int k1 = k;
         while (k1 < 8 && plan.order[k1] % 2 == q) ++k1;
-        for (int j = 0; j < 2; ++j) {
-            if (k > 0) PMC_HIP(hipStreamWaitEvent(st[j], c->ev_c[1 - j][1 - q], 0));   // the other's previous run
+        for (int j = 0; j < n; ++j) {
+            if (k > 0) {   // the neighbours' previous runs (one neighbour when there are two chains)
+                const int lo = (j + n - 1) % n, hi = (j + 1) % n;
+                PMC_HIP(hipStreamWaitEvent(st[j], c->ev_c[lo][1 - q], 0));
+                if (hi != lo) PMC_HIP(hipStreamWaitEvent(st[j], c->ev_c[hi][1 - q], 0));
+            }
             for (int kk = k; kk < k1; ++kk) {
                 int o[3];
                 pmc_colour_offset(plan.order[kk], o);
                 LaunchTiming lt;
                 hipError_t e = launch_subsweep(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep, c->stats,
-                                               ovf[j], j == 0 ? 0 : zs, j == 0 ? zs : nz, st[j],
+                                               ovf[j], chain_border(nz, n, j), chain_border(nz, n, j + 1), st[j],
                                                next_timing(c, 0, &lt, c->phase_seq + kk));
                 if (e != hipSuccess) return hip_fail(e, "subsweep launch");
             }
@@ -267,8 +286,8 @@ int enqueue_sweep_chains(pmc_ctx* c, uint32_t sweep, const pmc_sweep_plan_t& pla
         k = k1;
     }
     c->phase_seq += 8;
-    PMC_HIP(hipEventRecord(c->ev_s, c->hs));
-    PMC_HIP(hipStreamWaitEvent(c->stream, c->ev_s, 0));   // shiftCells reads every plane
+    for (int j = 1; j < n; ++j)   // shiftCells reads every plane: each chain's last run
+        PMC_HIP(hipStreamWaitEvent(c->stream, c->ev_c[j][q], 0));
     LaunchTiming lt;
     hipError_t e = launch_shift(c->G, c->disk[c->cur], c->n[c->cur], c->disk[c->cur ^ 1], c->n[c->cur ^ 1],
                                 plan.f, plan.d, c->flags, c->stream, next_timing(c, 1, &lt));
@@ -279,7 +298,8 @@ int enqueue_sweep_chains(pmc_ctx* c, uint32_t sweep, const pmc_sweep_plan_t& pla
 
 int enqueue_sweep(pmc_ctx* c, uint32_t sweep, bool chains = true) {
     const pmc_sweep_plan_t plan = pmc_plan_for_sweep_ex(c->P.seed, sweep, c->P.w, c->P.flags);
-    if (chains && !c->P.halo && chain_count(c) == 2) return enqueue_sweep_chains(c, sweep, plan);
+    const int n = chains ? chain_count(c) : 1;
+    if (n > 1) return enqueue_sweep_chains(c, sweep, plan, n);
     for (int k = 0; k < 8; ++k) {
         int o[3];
         pmc_colour_offset(plan.order[k], o);
@@ -394,12 +414,17 @@ void pmc_destroy(pmc_ctx* c) {
     if (c->tmp_idx) (void)hipFree(c->tmp_idx);
     if (c->d_r) (void)hipFree(c->d_r);
     for (hipEvent_t e : c->tev) (void)hipEventDestroy(e);
-    if (c->hs) {
-        (void)hipStreamSynchronize(c->hs);
-        (void)hipStreamDestroy(c->hs);
-    }
-    for (hipEvent_t e : {c->ev_c[0][0], c->ev_c[0][1], c->ev_c[1][0], c->ev_c[1][1], c->ev_s})
-        if (e) (void)hipEventDestroy(e);
+    for (hipStream_t h : c->hs)
+        if (h) {
+            (void)hipStreamSynchronize(h);
+            (void)hipStreamDestroy(h);
+        }
+    for (int* q : c->ovf_ch)
+        if (q) (void)hipFree(q);
+    for (auto& r : c->ev_c)
+        for (hipEvent_t e : r)
+            if (e) (void)hipEventDestroy(e);
+    if (c->ev_s) (void)hipEventDestroy(c->ev_s);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
@@ -1175,6 +1200,14 @@ struct pmc_slab {
     ncclComm_t comm = nullptr;            // RCCL transport
     pmc_local_group* group = nullptr;     // in-process transport (not owned)
     hipStream_t aux = nullptr;            // halo exchanges ("T")
+    // the sweep's LAST run exchange and the halo shift after it ("T2", x/y shifts): off the boundary
+    // chain, which starts the next sweep as soon as the shift is done unless its first boundary plane
+    // reads that halo.  xs: the stream the exchange being issued runs on (aux, or aux2 for that one).
+    hipStream_t aux2 = nullptr;
+    hipStream_t xs = nullptr;
+    hipEvent_t ev_t2 = nullptr;           // aux2 after its exchange and halo shift
+    bool t2_pending = false;              // aux2 work the exchange stream is not yet ordered after
+    int t2_parity = 0;                    // the parity of the halo aux2 fills (H_q: q of that exchange)
     hipStream_t hi[2] = {nullptr, nullptr};   // interior chains 1 and 2 (chain 0 runs on the context stream)
     int chains = 2;                       // interior plane chains (streams running subsweeps): 1, 2 or 3
     hipEvent_t ev_i = nullptr, ev_b = nullptr, ev_t = nullptr;
@@ -1226,6 +1259,7 @@ void drop_slab(pmc_ctx* c) {
     pmc_slab* s = c->slab;
     if (!s) return;
     (void)ipc_settle(c);   // (IPC: no peer still pulls from the buffers about to be freed)
+    if (s->aux2) (void)hipStreamSynchronize(s->aux2);
     if (s->aux) (void)hipStreamSynchronize(s->aux);
     if (s->comm && rccl().ok) (void)rccl().comm_destroy(s->comm);
     if (s->group) {
@@ -1233,6 +1267,8 @@ void drop_slab(pmc_ctx* c) {
         s->group->slot[s->rank].joined = false;
     }
     if (s->aux) (void)hipStreamDestroy(s->aux);
+    if (s->aux2) (void)hipStreamDestroy(s->aux2);
+    if (s->ev_t2) (void)hipEventDestroy(s->ev_t2);
     for (hipStream_t h : s->hi)
         if (h) (void)hipStreamSynchronize(h);
     if (s->stats_scratch) (void)hipFree(s->stats_scratch);   // (the send planes are the context's)
@@ -1275,7 +1311,7 @@ int slab_join(pmc_ctx* c) {
     pmc_slab* s = c->slab;
     if (!s) return PMC_OK;
     if (int rc = ipc_settle(c)) return rc;   // IPC: the peers are done reading this rank's buffers
-    for (hipStream_t st : {s->aux, s->hi[0], s->hi[1]}) {
+    for (hipStream_t st : {s->aux, s->aux2, s->hi[0], s->hi[1]}) {
         if (!st) continue;
         hipError_t e = hipEventRecord(s->ev_b, st);
         if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, s->ev_b, 0);
@@ -1370,7 +1406,7 @@ int ipc_run(pmc_ctx* c, const std::vector<XferMsg>& sends, const std::vector<Xfe
             s->pend_readers.push_back(m.peer);
     s->pend_seq = seq;
     hipError_t e = launch_xfer(cp, w, c->xflags + kFlagReady, c->xflags + kFlagPulled, seq,
-                               reinterpret_cast<unsigned*>(c->xflags + kFlagDone), s->ipc_timeout, c->flags, s->aux);
+                               reinterpret_cast<unsigned*>(c->xflags + kFlagDone), s->ipc_timeout, c->flags, s->xs);
     return e == hipSuccess ? PMC_OK : hip_fail(e, "IPC halo exchange");
 }
 
@@ -1385,7 +1421,18 @@ int ipc_settle(pmc_ctx* c) {
     return e == hipSuccess ? PMC_OK : hip_fail(e, "IPC settle");
 }
 
-// carry the queued messages on the aux stream (RCCL group, IPC pulls, or the in-process group's copies)
+// Exchanges complete in issue order on each rank (the IPC flags are monotonic, the halos they write are
+// the ones an earlier exchange or halo shift wrote): an exchange on aux first waits for pending aux2
+// work.  Called at the top of every exchange.
+int exchange_begin(pmc_slab* s) {
+    if (s->t2_pending && s->xs == s->aux) {
+        PMC_HIP(hipStreamWaitEvent(s->aux, s->ev_t2, 0));
+        s->t2_pending = false;
+    }
+    return PMC_OK;
+}
+
+// carry the queued messages on the exchange stream (RCCL group, IPC pulls, or the in-process group's copies)
 int xfer_run(pmc_ctx* c) {
     pmc_slab* s = c->slab;
     std::vector<XferMsg> sends, recvs;
@@ -1395,8 +1442,8 @@ int xfer_run(pmc_ctx* c) {
     if (s->comm) {
         Rccl& R = rccl();
         PMC_NCCL(R.group_start());
-        for (const XferMsg& m : sends) PMC_NCCL(R.send(m.buf, m.bytes, ncclUint8, m.peer, s->comm, s->aux));
-        for (const XferMsg& m : recvs) PMC_NCCL(R.recv(m.buf, m.bytes, ncclUint8, m.peer, s->comm, s->aux));
+        for (const XferMsg& m : sends) PMC_NCCL(R.send(m.buf, m.bytes, ncclUint8, m.peer, s->comm, s->xs));
+        for (const XferMsg& m : recvs) PMC_NCCL(R.recv(m.buf, m.bytes, ncclUint8, m.peer, s->comm, s->xs));
         PMC_NCCL(R.group_end());
         return PMC_OK;
     }
@@ -1404,7 +1451,7 @@ int xfer_run(pmc_ctx* c) {
     if (!g) return fail(PMC_ERR_ARG, "slab exchange without a transport");
     pmc_local_group::Slot& me = g->slot[s->rank];
     // 1. publish the send list and an event after the work that wrote the send buffers
-    hipError_t e = hipEventRecord(me.ready, s->aux);
+    hipError_t e = hipEventRecord(me.ready, s->xs);
     if (e != hipSuccess) { group_break(g); return hip_fail(e, "hipEventRecord"); }
     {
         std::lock_guard<std::mutex> lk(g->m);
@@ -1426,13 +1473,13 @@ int xfer_run(pmc_ctx* c) {
             return fail(PMC_ERR_ARG, "local group: unmatched or mis-sized halo message");
         }
         ++taken[m.peer];
-        if ((e = hipStreamWaitEvent(s->aux, src.ready, 0)) != hipSuccess ||
-            (e = hipMemcpyAsync(m.buf, hit->buf, m.bytes, hipMemcpyDeviceToDevice, s->aux)) != hipSuccess) {
+        if ((e = hipStreamWaitEvent(s->xs, src.ready, 0)) != hipSuccess ||
+            (e = hipMemcpyAsync(m.buf, hit->buf, m.bytes, hipMemcpyDeviceToDevice, s->xs)) != hipSuccess) {
             group_break(g);
             return hip_fail(e, "local group: halo copy");
         }
     }
-    if ((e = hipEventRecord(me.pulled, s->aux)) != hipSuccess) { group_break(g); return hip_fail(e, "hipEventRecord"); }
+    if ((e = hipEventRecord(me.pulled, s->xs)) != hipSuccess) { group_break(g); return hip_fail(e, "hipEventRecord"); }
     // every send must be received (the slots are stable between the two barriers: a rank publishes
     // its next lists only after the second one)
     std::vector<char> readers(g->world, 0);
@@ -1453,7 +1500,7 @@ int xfer_run(pmc_ctx* c) {
     //    exchange's first barrier, which this rank has not reached yet
     for (int p = 0; p < g->world; ++p) {
         if (!readers[p]) continue;
-        if ((e = hipStreamWaitEvent(s->aux, g->slot[p].pulled, 0)) != hipSuccess) {
+        if ((e = hipStreamWaitEvent(s->xs, g->slot[p].pulled, 0)) != hipSuccess) {
             group_break(g);
             return hip_fail(e, "hipStreamWaitEvent");
         }
@@ -1492,7 +1539,7 @@ double xfer_delay_us() {
 int inject_delay(pmc_slab* s) {
     const double us = xfer_delay_us();
     if (us <= 0.0) return PMC_OK;
-    hipError_t e = launch_spin(us, s->aux);
+    hipError_t e = launch_spin(us, s->xs);
     return e == hipSuccess ? PMC_OK : hip_fail(e, "injected exchange delay");
 }
 
@@ -1506,15 +1553,16 @@ int inject_delay(pmc_slab* s) {
 // without messages copies its own plane into its periodic halo.  On aux.
 int slab_exchange_run(pmc_ctx* c, int p, bool with_counts = false, bool rows_written = false) {
     pmc_slab* s = c->slab;
+    if (int rc = exchange_begin(s)) return rc;
     const int nz = c->P.nz_local;
     const size_t pf = plane_floats(c), pc = plane_cells(c);
     const int src = p == 0 ? 0 : nz - 1, dst = p == 0 ? nz : -1;
     if (!s->messages()) {
         // (rows_written: the boundary launches already wrote the rows into the halo: direct halo)
         if (!rows_written)
-            PMC_HIP(hipMemcpyAsync(disk_plane(c, dst), disk_plane(c, src), pf * 4, hipMemcpyDeviceToDevice, s->aux));
+            PMC_HIP(hipMemcpyAsync(disk_plane(c, dst), disk_plane(c, src), pf * 4, hipMemcpyDeviceToDevice, s->xs));
         if (with_counts)
-            PMC_HIP(hipMemcpyAsync(n_plane(c, dst), n_plane(c, src), pc * 2, hipMemcpyDeviceToDevice, s->aux));
+            PMC_HIP(hipMemcpyAsync(n_plane(c, dst), n_plane(c, src), pc * 2, hipMemcpyDeviceToDevice, s->xs));
         return inject_delay(s);
     }
     const int to = p == 0 ? s->below : s->above, from = p == 0 ? s->above : s->below;
@@ -1533,6 +1581,7 @@ int slab_exchange_run(pmc_ctx* c, int p, bool with_counts = false, bool rows_wri
 // nz-2 of the state).  On aux.
 int slab_exchange_full(pmc_ctx* c, bool from_send = false) {
     pmc_slab* s = c->slab;
+    if (int rc = exchange_begin(s)) return rc;
     const int nz = c->P.nz_local, h = c->P.halo;
     const size_t pf = plane_floats(c), pc = plane_cells(c);
     const float* lo_d = from_send ? s->send_d : disk_plane(c, 0);
@@ -1541,10 +1590,10 @@ int slab_exchange_full(pmc_ctx* c, bool from_send = false) {
     const int16_t* hi_n = from_send ? s->send_n + (size_t)h * pc : n_plane(c, nz - h);
     const size_t db = (size_t)h * pf * 4, nb = (size_t)h * pc * 2;
     if (!s->messages()) {
-        PMC_HIP(hipMemcpyAsync(disk_plane(c, nz), lo_d, db, hipMemcpyDeviceToDevice, s->aux));
-        PMC_HIP(hipMemcpyAsync(n_plane(c, nz), lo_n, nb, hipMemcpyDeviceToDevice, s->aux));
-        PMC_HIP(hipMemcpyAsync(disk_plane(c, -h), hi_d, db, hipMemcpyDeviceToDevice, s->aux));
-        PMC_HIP(hipMemcpyAsync(n_plane(c, -h), hi_n, nb, hipMemcpyDeviceToDevice, s->aux));
+        PMC_HIP(hipMemcpyAsync(disk_plane(c, nz), lo_d, db, hipMemcpyDeviceToDevice, s->xs));
+        PMC_HIP(hipMemcpyAsync(n_plane(c, nz), lo_n, nb, hipMemcpyDeviceToDevice, s->xs));
+        PMC_HIP(hipMemcpyAsync(disk_plane(c, -h), hi_d, db, hipMemcpyDeviceToDevice, s->xs));
+        PMC_HIP(hipMemcpyAsync(n_plane(c, -h), hi_n, nb, hipMemcpyDeviceToDevice, s->xs));
         return PMC_OK;
     }
     // per peer, sends and receives match in issue order: (planes, counts) down, then up
@@ -1564,12 +1613,13 @@ int slab_exchange_full(pmc_ctx* c, bool from_send = false) {
 // plane next to it (the -dir side was shifted locally), on aux
 int slab_exchange_zplane(pmc_ctx* c, int dir) {
     pmc_slab* s = c->slab;
+    if (int rc = exchange_begin(s)) return rc;
     const int nz = c->P.nz_local;
     const size_t pf = plane_floats(c), pc = plane_cells(c);
     const int src = dir > 0 ? 0 : nz - 1, dst = dir > 0 ? nz : -1;   // my plane -> the -dir rank's halo
     if (!s->messages()) {
-        PMC_HIP(hipMemcpyAsync(disk_plane(c, dst), disk_plane(c, src), pf * 4, hipMemcpyDeviceToDevice, s->aux));
-        PMC_HIP(hipMemcpyAsync(n_plane(c, dst), n_plane(c, src), pc * 2, hipMemcpyDeviceToDevice, s->aux));
+        PMC_HIP(hipMemcpyAsync(disk_plane(c, dst), disk_plane(c, src), pf * 4, hipMemcpyDeviceToDevice, s->xs));
+        PMC_HIP(hipMemcpyAsync(n_plane(c, dst), n_plane(c, src), pc * 2, hipMemcpyDeviceToDevice, s->xs));
         return inject_delay(s);
     }
     const int to = dir > 0 ? s->below : s->above, from = dir > 0 ? s->above : s->below;
@@ -1638,10 +1688,13 @@ int slab_attach(pmc_ctx* c, int rank, int world, bool messages) {
     }();
     int lo_p = 0, hi_p = 0;
     if (prio) (void)hipDeviceGetStreamPriorityRange(&lo_p, &hi_p);
-    if ((e = hipStreamCreateWithPriority(&s->aux, hipStreamNonBlocking, prio ? hi_p : 0)) != hipSuccess) {
+    if ((e = hipStreamCreateWithPriority(&s->aux, hipStreamNonBlocking, prio ? hi_p : 0)) != hipSuccess ||
+        (e = hipStreamCreateWithPriority(&s->aux2, hipStreamNonBlocking, prio ? hi_p : 0)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&s->ev_t2, hipEventDisableTiming)) != hipSuccess) {
         drop_slab(c);
         return hip_fail(e, "hipStreamCreate");
     }
+    s->xs = s->aux;
     std::vector<hipEvent_t*> evs = {&s->ev_i, &s->ev_b, &s->ev_t, &s->ev_x, &s->ev_hp};
     for (hipEvent_t* ev : s->run_events()) evs.push_back(ev);
     for (hipEvent_t* ev : evs)
@@ -2124,6 +2177,25 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
     int* iovf[3] = {c->ovf, c->ovf_aux, c->ovf_aux2};
     const pmc_sweep_plan_t plan = pmc_plan_for_sweep_ex(c->P.seed, sweep, c->P.w, c->P.flags);
     int rc;
+    // Split shift (default; PMC_SLAB_SPLIT_SHIFT=0 off; shifts along x or y, below), with PMC_SLAB_T2=1:
+    // the LAST run's exchange and the shift of the halo it fills go on a second exchange stream (aux2)
+    // instead of T, so T -- the boundary chain -- starts the next sweep as soon as shiftCells is done, unless the
+    // next sweep's first boundary plane reads that halo (then it waits for aux2)
+    static const bool split_env = [] {   // default on (PMC_SLAB_SPLIT_SHIFT=0: off)
+        const char* v = std::getenv("PMC_SLAB_SPLIT_SHIFT");
+        return !(v && std::atoi(v) == 0);
+    }();
+    static const bool t2_env = [] {   // PMC_SLAB_T2=1: the last exchange and its halo shift on aux2
+        const char* v = std::getenv("PMC_SLAB_T2");
+        return v && std::atoi(v) == 1;
+    }();
+    const bool t2 = t2_env && split_env && plan.f != 2;
+    // the previous sweep's last exchange and halo shift on aux2: this sweep's first boundary plane
+    // waits for them if it reads that halo (parity 1 - first parity)
+    if (s->t2_pending && 1 - plan.order[0] % 2 == s->t2_parity) {
+        PMC_HIP(hipStreamWaitEvent(T, s->ev_t2, 0));
+        s->t2_pending = false;
+    }
     // a deferred z-shift halo exchange: carried by this sweep's first run exchange when this is the
     // sweep it was deferred to (the first run's boundary plane does not read that halo), else now
     bool merge_z = false;
@@ -2221,7 +2293,15 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
             if (!first && (r = border_waits(kB, zb, zb + 1, q, T, p))) return r;
             if ((r = phases(T, c->ovf_b, zb, zb + 1, k, k1, true))) return r;
             PMC_HIP(hipEventRecord(s->ev_run[kB][q], T));
-            if ((r = slab_exchange_run(c, q, merge_z, direct_halo))) return r;
+            if (t2 && k1 == 8) {   // the sweep's last exchange on aux2, after this run's boundary phases
+                PMC_HIP(hipStreamWaitEvent(s->aux2, s->ev_run[kB][q], 0));
+                s->xs = s->aux2;
+                r = slab_exchange_run(c, q, merge_z, direct_halo);
+                s->xs = s->aux;
+                if (r) return r;
+            } else if ((r = slab_exchange_run(c, q, merge_z, direct_halo))) {
+                return r;
+            }
             merge_z = false;
             s->pending_zdir = 0;
             return PMC_OK;
@@ -2251,10 +2331,6 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
     // shifts H_q after it: the exchange leaves the sweep's critical path (it matters once the
     // exchange takes xGMI time: PMC_XFER_DELAY_US rehearsals).  The next sweep's interior chains
     // read no halo; T, which runs the next boundary phases, is in order after its own part.
-    static const bool split_env = [] {   // default on (PMC_SLAB_SPLIT_SHIFT=0: off)
-        const char* v = std::getenv("PMC_SLAB_SPLIT_SHIFT");
-        return !(v && std::atoi(v) == 0);
-    }();
     const int q_last = plan.order[7] % 2;
     const int hq = q_last == 0 ? nz : -1;                    // the halo the last exchange fills
     const bool split = split_env && plan.f != 2 && hq >= zl0 && hq < zl1;
@@ -2271,9 +2347,15 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
         e = launch_shift_planes(c->G, c->disk[c->cur], c->n[c->cur], c->disk[c->cur ^ 1], c->n[c->cur ^ 1], plan.f,
                                 plan.d, c->flags, a0, a1, S, next_timing(c, 1, &lts));
         if (e != hipSuccess) return hip_fail(e, "shift launch");
+        // the halo the last exchange fills: shifted where that exchange ran (aux2 with t2, else T)
         e = launch_shift_planes(c->G, c->disk[c->cur], c->n[c->cur], c->disk[c->cur ^ 1], c->n[c->cur ^ 1], plan.f,
-                                plan.d, c->flags, hq, hq + 1, T, nullptr);
+                                plan.d, c->flags, hq, hq + 1, t2 ? s->aux2 : T, nullptr);
         if (e != hipSuccess) return hip_fail(e, "shift launch (halo)");
+        if (t2) {
+            PMC_HIP(hipEventRecord(s->ev_t2, s->aux2));
+            s->t2_pending = true;
+            s->t2_parity = q_last;
+        }
     } else {
         // shiftCells reads every plane and both halos: the other chains and T joined into S
         PMC_HIP(hipEventRecord(s->ev_x, T));
@@ -2341,6 +2423,7 @@ int pmc_slab_observables(pmc_ctx* c, int with_energy, pmc_stats* out, double* e_
     // two's-complement sums: exact for the signed fields as 64-bit unsigned sums
     uint64_t v[5] = {(uint64_t)st.de_fixed, (uint64_t)st.accepted, (uint64_t)st.trials, (uint64_t)st.evaluated,
                      (uint64_t)ef};
+    if (int rc = exchange_begin(s)) return rc;   // (after the last sweep's exchange on aux2)
     if (s->comm) {
         Rccl& R = rccl();
         if (!R.all_reduce) return fail(PMC_ERR_HIP, "librccl lacks ncclAllReduce");
@@ -2420,7 +2503,8 @@ int pmc_timing_kinds(pmc_ctx* c, int enable, double ms[3], int count[3]) {
         if (c->slab)
             for (hipStream_t h : c->slab->hi)
                 if (h) PMC_HIP(hipStreamSynchronize(h));
-        if (c->hs) PMC_HIP(hipStreamSynchronize(c->hs));
+        for (hipStream_t h : c->hs)
+            if (h) PMC_HIP(hipStreamSynchronize(h));
         for (size_t k = 0; k < c->tkind.size(); ++k) {
             float t = 0.0f;
             PMC_HIP(hipEventElapsedTime(&t, c->tev[2 * k], c->tev[2 * k + 1]));
@@ -2467,13 +2551,11 @@ int pmc_timing_phase_spans(pmc_ctx* c, double* span_ms, int* n_phases) {
     return PMC_OK;
 }
 
-int pmc_sweep_layout(pmc_ctx* c, int* n_chains, int borders[3]) {
+int pmc_sweep_layout(pmc_ctx* c, int* n_chains, int borders[PMC_SWEEP_MAX_CHAINS + 1]) {
     if (!c || !n_chains || !borders) return fail(PMC_ERR_ARG, "null argument");
     const int nz = c->P.nz_local;
-    *n_chains = (!c->P.halo && chain_count(c) == 2) ? 2 : 1;
-    borders[0] = 0;
-    borders[1] = *n_chains == 2 ? 2 * (nz / 4) : nz;
-    borders[2] = nz;
+    *n_chains = chain_count(c);
+    for (int j = 0; j <= PMC_SWEEP_MAX_CHAINS; ++j) borders[j] = j <= *n_chains ? chain_border(nz, *n_chains, j) : nz;
     return PMC_OK;
 }
 

@@ -131,7 +131,7 @@ def lib():
         _sig(L, "pmc_timing_kinds", i32, _vp, i32, C.POINTER(C.c_double * 3), C.POINTER(C.c_int * 3))
         _sig(L, "pmc_timing_pause", i32, _vp, i32)
         _sig(L, "pmc_timing_phase_spans", i32, _vp, C.POINTER(C.c_double), C.POINTER(C.c_int))
-        _sig(L, "pmc_sweep_layout", i32, _vp, C.POINTER(C.c_int), C.POINTER(C.c_int * 3))
+        _sig(L, "pmc_sweep_layout", i32, _vp, C.POINTER(C.c_int), C.POINTER(C.c_int * 5))
         _sig(L, "pmc_subsweep_range", i32, _vp, _vp, _vp, C.POINTER(C.c_int * 3), u32, i32, i32)
         _sig(L, "pmc_shift", i32, _vp, u32)
         _sig(L, "pmc_shift_slab", i32, _vp, u32, _vp)

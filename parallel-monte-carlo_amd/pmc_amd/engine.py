@@ -250,7 +250,7 @@ class PmcContext:
     def sweep_layout(self) -> list:
         """pmc_sweep's plane chains as (first plane, end plane) pairs (pmc_sweep_layout)."""
         n = C.c_int(0)
-        b = (C.c_int * 3)()
+        b = (C.c_int * 5)()   # PMC_SWEEP_MAX_CHAINS + 1
         check("pmc_sweep_layout", lib().pmc_sweep_layout(self._h, C.byref(n), C.byref(b)))
         return [(b[j], b[j + 1]) for j in range(n.value)]
 

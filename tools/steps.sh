@@ -16,6 +16,8 @@
 #                    default local), injected exchange delay us
 #   mp2bench         bench.py --gpus 2 --same-device --config 4 (rank processes, IPC)
 #   rocprof          rocprofv3 --kernel-trace --stats of the default bench command
+#   tcc | sq | shcnt  counter passes: k_subsweep traffic (tools/tcc_traffic.sh), its SQ instruction mix
+#                    (tools/sq_counters.sh), k_shift traffic + wave states (tools/shift_counters.sh)
 # A step may carry environment variables: PMC_QUAD_CELLS=40000@bench2 (A/B switches).
 set -o pipefail
 TAG=${1:?tag}; shift
@@ -70,6 +72,9 @@ for spec in "$@"; do
                 --rank-timeout 360 > $log 2>&1 ;;
         rocprof) export TMPDIR=/tmp; timeout -k 10 400 rocprofv3 --kernel-trace --stats \
                 -d $OUT/rocprof -o bench -- python3 bench.py --steps 20 --warmup 5 > $log 2>&1 ;;
+        tcc) timeout -k 10 600 bash tools/tcc_traffic.sh $TAG > $log 2>&1 ;;
+        sq) timeout -k 10 500 bash tools/sq_counters.sh $TAG > $log 2>&1 ;;
+        shcnt) timeout -k 10 700 bash tools/shift_counters.sh $TAG > $log 2>&1 ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
     rc=$?
@@ -77,6 +82,8 @@ for spec in "$@"; do
     if [ $rc -ne 0 ]; then echo "step $spec failed rc $rc"; tail -40 $log; exit $rc; fi
     case $step in
         tests*|mp|smoke) tail -1 $log ;;
+        tcc|sq|shcnt) tail -12 $log ;;
+        rocprof) python3 tools/rocprof_timed_mean.py $OUT/rocprof 2>&1 | tail -8 ;;
         *) grep '^{' $log > $OUT/$name.json; summ $OUT/$name.json ;;
     esac
 done
