@@ -611,8 +611,9 @@ def main() -> int:
         stencil = stencil_counts(n_owned, (cps, cps, cps))
         phase_bytes = staged_bytes(n_owned, stencil) / 8.0
         # pmc_sweep's plane chains (pmc_sweep_layout): each colour phase is one launch per chain, the
-        # chains' launches concurrent; the roofline is per PHASE (its span: earliest launch start to
-        # latest stop, HIP events on the dispatch packets), launch_ms the per-launch mean
+        # chains' launches concurrent and a chain's next phase overlapping the others' tails; the
+        # roofline is per PHASE: a timed sweep's subsweep span (first launch start to last stop, HIP
+        # events on the dispatch packets; gaps included, shiftCells not) / 8, launch_ms the per-launch mean
         sweep_chains = sim.sweep_layout()
         per_chain = [staged_bytes(n_owned[a * plane:b * plane], stencil[a * plane:b * plane]) / 8.0
                      for a, b in sweep_chains]
@@ -620,7 +621,7 @@ def main() -> int:
         roof_kernel = ("k_subsweep<16,16,true> (one colour phase of the whole box" +
                        (f" as {len(sweep_chains)} concurrent launches, plane chains " +
                         " and ".join(f"[{a},{b})" for a, b in sweep_chains) +
-                        "; achieved/frac per phase over its span" if len(sweep_chains) > 1 else "") + ")")
+                        "; achieved/frac per phase: a sweep's subsweep span / 8" if len(sweep_chains) > 1 else "") + ")")
     else:
         n_owned = n_h[plane * drv.halo:plane * (nz_local + drv.halo)].astype(np.int64)
         stencil = slab_stencil_counts(n_h, cps, nz_local, drv.halo)

@@ -264,8 +264,10 @@ int pmc_slab_observables(pmc_ctx* ctx, int with_energy, pmc_stats* out, double* 
 int pmc_timing(pmc_ctx* ctx, int enable, double* subsweep_ms, int* n_subsweep, double* shift_ms, int* n_shift);
 int pmc_timing_kinds(pmc_ctx* ctx, int enable, double ms[3], int count[3]);
 /* Colour phases that pmc_sweep splits over plane chains (pmc_sweep_layout) run as concurrent
- * launches: the last pmc_timing / pmc_timing_kinds call also summed each such phase's span, from its
- * earliest launch start to its latest stop; this returns that sum and the number of phases. */
+ * launches, a chain starting its next phase while the others finish theirs: the last pmc_timing /
+ * pmc_timing_kinds call also summed, per timed sweep, the span of its subsweep launches (first start
+ * to last stop: the 8 phases with the gaps between them, shiftCells excluded); this returns that sum
+ * and the number of phases it covers (8 per sweep). */
 int pmc_timing_phase_spans(pmc_ctx* ctx, double* span_ms, int* n_phases);
 /* pmc_sweep's plane chains (whole box): *n_chains (1, 2 or 4: PMC_SWEEP_CHAINS, default 2; fewer when
  * the box has under 4 planes per chain), chain j over local planes [borders[j], borders[j+1]) (entries

@@ -1200,14 +1200,6 @@ struct pmc_slab {
     ncclComm_t comm = nullptr;            // RCCL transport
     pmc_local_group* group = nullptr;     // in-process transport (not owned)
     hipStream_t aux = nullptr;            // halo exchanges ("T")
-    // the sweep's LAST run exchange and the halo shift after it ("T2", x/y shifts): off the boundary
-    // chain, which starts the next sweep as soon as the shift is done unless its first boundary plane
-    // reads that halo.  xs: the stream the exchange being issued runs on (aux, or aux2 for that one).
-    hipStream_t aux2 = nullptr;
-    hipStream_t xs = nullptr;
-    hipEvent_t ev_t2 = nullptr;           // aux2 after its exchange and halo shift
-    bool t2_pending = false;              // aux2 work the exchange stream is not yet ordered after
-    int t2_parity = 0;                    // the parity of the halo aux2 fills (H_q: q of that exchange)
     hipStream_t hi[2] = {nullptr, nullptr};   // interior chains 1 and 2 (chain 0 runs on the context stream)
     int chains = 2;                       // interior plane chains (streams running subsweeps): 1, 2 or 3
     hipEvent_t ev_i = nullptr, ev_b = nullptr, ev_t = nullptr;
@@ -1259,7 +1251,6 @@ void drop_slab(pmc_ctx* c) {
     pmc_slab* s = c->slab;
     if (!s) return;
     (void)ipc_settle(c);   // (IPC: no peer still pulls from the buffers about to be freed)
-    if (s->aux2) (void)hipStreamSynchronize(s->aux2);
     if (s->aux) (void)hipStreamSynchronize(s->aux);
     if (s->comm && rccl().ok) (void)rccl().comm_destroy(s->comm);
     if (s->group) {
@@ -1267,8 +1258,6 @@ void drop_slab(pmc_ctx* c) {
         s->group->slot[s->rank].joined = false;
     }
     if (s->aux) (void)hipStreamDestroy(s->aux);
-    if (s->aux2) (void)hipStreamDestroy(s->aux2);
-    if (s->ev_t2) (void)hipEventDestroy(s->ev_t2);
     for (hipStream_t h : s->hi)
         if (h) (void)hipStreamSynchronize(h);
     if (s->stats_scratch) (void)hipFree(s->stats_scratch);   // (the send planes are the context's)
@@ -1311,7 +1300,7 @@ int slab_join(pmc_ctx* c) {
     pmc_slab* s = c->slab;
     if (!s) return PMC_OK;
     if (int rc = ipc_settle(c)) return rc;   // IPC: the peers are done reading this rank's buffers
-    for (hipStream_t st : {s->aux, s->aux2, s->hi[0], s->hi[1]}) {
+    for (hipStream_t st : {s->aux, s->hi[0], s->hi[1]}) {
         if (!st) continue;
         hipError_t e = hipEventRecord(s->ev_b, st);
         if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, s->ev_b, 0);
@@ -1406,7 +1395,7 @@ int ipc_run(pmc_ctx* c, const std::vector<XferMsg>& sends, const std::vector<Xfe
             s->pend_readers.push_back(m.peer);
     s->pend_seq = seq;
     hipError_t e = launch_xfer(cp, w, c->xflags + kFlagReady, c->xflags + kFlagPulled, seq,
-                               reinterpret_cast<unsigned*>(c->xflags + kFlagDone), s->ipc_timeout, c->flags, s->xs);
+                               reinterpret_cast<unsigned*>(c->xflags + kFlagDone), s->ipc_timeout, c->flags, s->aux);
     return e == hipSuccess ? PMC_OK : hip_fail(e, "IPC halo exchange");
 }
 
@@ -1421,18 +1410,7 @@ int ipc_settle(pmc_ctx* c) {
     return e == hipSuccess ? PMC_OK : hip_fail(e, "IPC settle");
 }
 
-// Exchanges complete in issue order on each rank (the IPC flags are monotonic, the halos they write are
-// the ones an earlier exchange or halo shift wrote): an exchange on aux first waits for pending aux2
-// work.  Called at the top of every exchange.
-int exchange_begin(pmc_slab* s) {
-    if (s->t2_pending && s->xs == s->aux) {
-        PMC_HIP(hipStreamWaitEvent(s->aux, s->ev_t2, 0));
-        s->t2_pending = false;
-    }
-    return PMC_OK;
-}
-
-// carry the queued messages on the exchange stream (RCCL group, IPC pulls, or the in-process group's copies)
+// carry the queued messages on the aux stream (RCCL group, IPC pulls, or the in-process group's copies)
 int xfer_run(pmc_ctx* c) {
     pmc_slab* s = c->slab;
     std::vector<XferMsg> sends, recvs;
@@ -1442,8 +1420,8 @@ int xfer_run(pmc_ctx* c) {
     if (s->comm) {
         Rccl& R = rccl();
         PMC_NCCL(R.group_start());
-        for (const XferMsg& m : sends) PMC_NCCL(R.send(m.buf, m.bytes, ncclUint8, m.peer, s->comm, s->xs));
-        for (const XferMsg& m : recvs) PMC_NCCL(R.recv(m.buf, m.bytes, ncclUint8, m.peer, s->comm, s->xs));
+        for (const XferMsg& m : sends) PMC_NCCL(R.send(m.buf, m.bytes, ncclUint8, m.peer, s->comm, s->aux));
+        for (const XferMsg& m : recvs) PMC_NCCL(R.recv(m.buf, m.bytes, ncclUint8, m.peer, s->comm, s->aux));
         PMC_NCCL(R.group_end());
         return PMC_OK;
     }
@@ -1451,7 +1429,7 @@ int xfer_run(pmc_ctx* c) {
     if (!g) return fail(PMC_ERR_ARG, "slab exchange without a transport");
     pmc_local_group::Slot& me = g->slot[s->rank];
     // 1. publish the send list and an event after the work that wrote the send buffers
-    hipError_t e = hipEventRecord(me.ready, s->xs);
+    hipError_t e = hipEventRecord(me.ready, s->aux);
     if (e != hipSuccess) { group_break(g); return hip_fail(e, "hipEventRecord"); }
     {
         std::lock_guard<std::mutex> lk(g->m);
@@ -1473,13 +1451,13 @@ int xfer_run(pmc_ctx* c) {
             return fail(PMC_ERR_ARG, "local group: unmatched or mis-sized halo message");
         }
         ++taken[m.peer];
-        if ((e = hipStreamWaitEvent(s->xs, src.ready, 0)) != hipSuccess ||
-            (e = hipMemcpyAsync(m.buf, hit->buf, m.bytes, hipMemcpyDeviceToDevice, s->xs)) != hipSuccess) {
+        if ((e = hipStreamWaitEvent(s->aux, src.ready, 0)) != hipSuccess ||
+            (e = hipMemcpyAsync(m.buf, hit->buf, m.bytes, hipMemcpyDeviceToDevice, s->aux)) != hipSuccess) {
             group_break(g);
             return hip_fail(e, "local group: halo copy");
         }
     }
-    if ((e = hipEventRecord(me.pulled, s->xs)) != hipSuccess) { group_break(g); return hip_fail(e, "hipEventRecord"); }
+    if ((e = hipEventRecord(me.pulled, s->aux)) != hipSuccess) { group_break(g); return hip_fail(e, "hipEventRecord"); }
     // every send must be received (the slots are stable between the two barriers: a rank publishes
     // its next lists only after the second one)
     std::vector<char> readers(g->world, 0);
@@ -1500,7 +1478,7 @@ int xfer_run(pmc_ctx* c) {
     //    exchange's first barrier, which this rank has not reached yet
     for (int p = 0; p < g->world; ++p) {
         if (!readers[p]) continue;
-        if ((e = hipStreamWaitEvent(s->xs, g->slot[p].pulled, 0)) != hipSuccess) {
+        if ((e = hipStreamWaitEvent(s->aux, g->slot[p].pulled, 0)) != hipSuccess) {
             group_break(g);
             return hip_fail(e, "hipStreamWaitEvent");
         }
@@ -1539,7 +1517,7 @@ double xfer_delay_us() {
 int inject_delay(pmc_slab* s) {
     const double us = xfer_delay_us();
     if (us <= 0.0) return PMC_OK;
-    hipError_t e = launch_spin(us, s->xs);
+    hipError_t e = launch_spin(us, s->aux);
     return e == hipSuccess ? PMC_OK : hip_fail(e, "injected exchange delay");
 }
 
@@ -1553,16 +1531,15 @@ int inject_delay(pmc_slab* s) {
 // without messages copies its own plane into its periodic halo.  On aux.
 int slab_exchange_run(pmc_ctx* c, int p, bool with_counts = false, bool rows_written = false) {
     pmc_slab* s = c->slab;
-    if (int rc = exchange_begin(s)) return rc;
     const int nz = c->P.nz_local;
     const size_t pf = plane_floats(c), pc = plane_cells(c);
     const int src = p == 0 ? 0 : nz - 1, dst = p == 0 ? nz : -1;
     if (!s->messages()) {
         // (rows_written: the boundary launches already wrote the rows into the halo: direct halo)
         if (!rows_written)
-            PMC_HIP(hipMemcpyAsync(disk_plane(c, dst), disk_plane(c, src), pf * 4, hipMemcpyDeviceToDevice, s->xs));
+            PMC_HIP(hipMemcpyAsync(disk_plane(c, dst), disk_plane(c, src), pf * 4, hipMemcpyDeviceToDevice, s->aux));
         if (with_counts)
-            PMC_HIP(hipMemcpyAsync(n_plane(c, dst), n_plane(c, src), pc * 2, hipMemcpyDeviceToDevice, s->xs));
+            PMC_HIP(hipMemcpyAsync(n_plane(c, dst), n_plane(c, src), pc * 2, hipMemcpyDeviceToDevice, s->aux));
         return inject_delay(s);
     }
     const int to = p == 0 ? s->below : s->above, from = p == 0 ? s->above : s->below;
@@ -1581,7 +1558,6 @@ int slab_exchange_run(pmc_ctx* c, int p, bool with_counts = false, bool rows_wri
 // nz-2 of the state).  On aux.
 int slab_exchange_full(pmc_ctx* c, bool from_send = false) {
     pmc_slab* s = c->slab;
-    if (int rc = exchange_begin(s)) return rc;
     const int nz = c->P.nz_local, h = c->P.halo;
     const size_t pf = plane_floats(c), pc = plane_cells(c);
     const float* lo_d = from_send ? s->send_d : disk_plane(c, 0);
@@ -1590,10 +1566,10 @@ int slab_exchange_full(pmc_ctx* c, bool from_send = false) {
     const int16_t* hi_n = from_send ? s->send_n + (size_t)h * pc : n_plane(c, nz - h);
     const size_t db = (size_t)h * pf * 4, nb = (size_t)h * pc * 2;
     if (!s->messages()) {
-        PMC_HIP(hipMemcpyAsync(disk_plane(c, nz), lo_d, db, hipMemcpyDeviceToDevice, s->xs));
-        PMC_HIP(hipMemcpyAsync(n_plane(c, nz), lo_n, nb, hipMemcpyDeviceToDevice, s->xs));
-        PMC_HIP(hipMemcpyAsync(disk_plane(c, -h), hi_d, db, hipMemcpyDeviceToDevice, s->xs));
-        PMC_HIP(hipMemcpyAsync(n_plane(c, -h), hi_n, nb, hipMemcpyDeviceToDevice, s->xs));
+        PMC_HIP(hipMemcpyAsync(disk_plane(c, nz), lo_d, db, hipMemcpyDeviceToDevice, s->aux));
+        PMC_HIP(hipMemcpyAsync(n_plane(c, nz), lo_n, nb, hipMemcpyDeviceToDevice, s->aux));
+        PMC_HIP(hipMemcpyAsync(disk_plane(c, -h), hi_d, db, hipMemcpyDeviceToDevice, s->aux));
+        PMC_HIP(hipMemcpyAsync(n_plane(c, -h), hi_n, nb, hipMemcpyDeviceToDevice, s->aux));
         return PMC_OK;
     }
     // per peer, sends and receives match in issue order: (planes, counts) down, then up
@@ -1613,13 +1589,12 @@ int slab_exchange_full(pmc_ctx* c, bool from_send = false) {
 // plane next to it (the -dir side was shifted locally), on aux
 int slab_exchange_zplane(pmc_ctx* c, int dir) {
     pmc_slab* s = c->slab;
-    if (int rc = exchange_begin(s)) return rc;
     const int nz = c->P.nz_local;
     const size_t pf = plane_floats(c), pc = plane_cells(c);
     const int src = dir > 0 ? 0 : nz - 1, dst = dir > 0 ? nz : -1;   // my plane -> the -dir rank's halo
     if (!s->messages()) {
-        PMC_HIP(hipMemcpyAsync(disk_plane(c, dst), disk_plane(c, src), pf * 4, hipMemcpyDeviceToDevice, s->xs));
-        PMC_HIP(hipMemcpyAsync(n_plane(c, dst), n_plane(c, src), pc * 2, hipMemcpyDeviceToDevice, s->xs));
+        PMC_HIP(hipMemcpyAsync(disk_plane(c, dst), disk_plane(c, src), pf * 4, hipMemcpyDeviceToDevice, s->aux));
+        PMC_HIP(hipMemcpyAsync(n_plane(c, dst), n_plane(c, src), pc * 2, hipMemcpyDeviceToDevice, s->aux));
         return inject_delay(s);
     }
     const int to = dir > 0 ? s->below : s->above, from = dir > 0 ? s->above : s->below;
@@ -1688,13 +1663,10 @@ int slab_attach(pmc_ctx* c, int rank, int world, bool messages) {
     }();
     int lo_p = 0, hi_p = 0;
     if (prio) (void)hipDeviceGetStreamPriorityRange(&lo_p, &hi_p);
-    if ((e = hipStreamCreateWithPriority(&s->aux, hipStreamNonBlocking, prio ? hi_p : 0)) != hipSuccess ||
-        (e = hipStreamCreateWithPriority(&s->aux2, hipStreamNonBlocking, prio ? hi_p : 0)) != hipSuccess ||
-        (e = hipEventCreateWithFlags(&s->ev_t2, hipEventDisableTiming)) != hipSuccess) {
+    if ((e = hipStreamCreateWithPriority(&s->aux, hipStreamNonBlocking, prio ? hi_p : 0)) != hipSuccess) {
         drop_slab(c);
         return hip_fail(e, "hipStreamCreate");
     }
-    s->xs = s->aux;
     std::vector<hipEvent_t*> evs = {&s->ev_i, &s->ev_b, &s->ev_t, &s->ev_x, &s->ev_hp};
     for (hipEvent_t* ev : s->run_events()) evs.push_back(ev);
     for (hipEvent_t* ev : evs)
@@ -2177,25 +2149,6 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
     int* iovf[3] = {c->ovf, c->ovf_aux, c->ovf_aux2};
     const pmc_sweep_plan_t plan = pmc_plan_for_sweep_ex(c->P.seed, sweep, c->P.w, c->P.flags);
     int rc;
-    // Split shift (default; PMC_SLAB_SPLIT_SHIFT=0 off; shifts along x or y, below), with PMC_SLAB_T2=1:
-    // the LAST run's exchange and the shift of the halo it fills go on a second exchange stream (aux2)
-    // instead of T, so T -- the boundary chain -- starts the next sweep as soon as shiftCells is done, unless the
-    // next sweep's first boundary plane reads that halo (then it waits for aux2)
-    static const bool split_env = [] {   // default on (PMC_SLAB_SPLIT_SHIFT=0: off)
-        const char* v = std::getenv("PMC_SLAB_SPLIT_SHIFT");
-        return !(v && std::atoi(v) == 0);
-    }();
-    static const bool t2_env = [] {   // PMC_SLAB_T2=1: the last exchange and its halo shift on aux2
-        const char* v = std::getenv("PMC_SLAB_T2");
-        return v && std::atoi(v) == 1;
-    }();
-    const bool t2 = t2_env && split_env && plan.f != 2;
-    // the previous sweep's last exchange and halo shift on aux2: this sweep's first boundary plane
-    // waits for them if it reads that halo (parity 1 - first parity)
-    if (s->t2_pending && 1 - plan.order[0] % 2 == s->t2_parity) {
-        PMC_HIP(hipStreamWaitEvent(T, s->ev_t2, 0));
-        s->t2_pending = false;
-    }
     // a deferred z-shift halo exchange: carried by this sweep's first run exchange when this is the
     // sweep it was deferred to (the first run's boundary plane does not read that halo), else now
     bool merge_z = false;
@@ -2293,15 +2246,7 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
             if (!first && (r = border_waits(kB, zb, zb + 1, q, T, p))) return r;
             if ((r = phases(T, c->ovf_b, zb, zb + 1, k, k1, true))) return r;
             PMC_HIP(hipEventRecord(s->ev_run[kB][q], T));
-            if (t2 && k1 == 8) {   // the sweep's last exchange on aux2, after this run's boundary phases
-                PMC_HIP(hipStreamWaitEvent(s->aux2, s->ev_run[kB][q], 0));
-                s->xs = s->aux2;
-                r = slab_exchange_run(c, q, merge_z, direct_halo);
-                s->xs = s->aux;
-                if (r) return r;
-            } else if ((r = slab_exchange_run(c, q, merge_z, direct_halo))) {
-                return r;
-            }
+            if ((r = slab_exchange_run(c, q, merge_z, direct_halo))) return r;
             merge_z = false;
             s->pending_zdir = 0;
             return PMC_OK;
@@ -2331,6 +2276,10 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
     // shifts H_q after it: the exchange leaves the sweep's critical path (it matters once the
     // exchange takes xGMI time: PMC_XFER_DELAY_US rehearsals).  The next sweep's interior chains
     // read no halo; T, which runs the next boundary phases, is in order after its own part.
+    static const bool split_env = [] {   // default on (PMC_SLAB_SPLIT_SHIFT=0: off)
+        const char* v = std::getenv("PMC_SLAB_SPLIT_SHIFT");
+        return !(v && std::atoi(v) == 0);
+    }();
     const int q_last = plan.order[7] % 2;
     const int hq = q_last == 0 ? nz : -1;                    // the halo the last exchange fills
     const bool split = split_env && plan.f != 2 && hq >= zl0 && hq < zl1;
@@ -2347,15 +2296,9 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
         e = launch_shift_planes(c->G, c->disk[c->cur], c->n[c->cur], c->disk[c->cur ^ 1], c->n[c->cur ^ 1], plan.f,
                                 plan.d, c->flags, a0, a1, S, next_timing(c, 1, &lts));
         if (e != hipSuccess) return hip_fail(e, "shift launch");
-        // the halo the last exchange fills: shifted where that exchange ran (aux2 with t2, else T)
         e = launch_shift_planes(c->G, c->disk[c->cur], c->n[c->cur], c->disk[c->cur ^ 1], c->n[c->cur ^ 1], plan.f,
-                                plan.d, c->flags, hq, hq + 1, t2 ? s->aux2 : T, nullptr);
+                                plan.d, c->flags, hq, hq + 1, T, nullptr);
         if (e != hipSuccess) return hip_fail(e, "shift launch (halo)");
-        if (t2) {
-            PMC_HIP(hipEventRecord(s->ev_t2, s->aux2));
-            s->t2_pending = true;
-            s->t2_parity = q_last;
-        }
     } else {
         // shiftCells reads every plane and both halos: the other chains and T joined into S
         PMC_HIP(hipEventRecord(s->ev_x, T));
@@ -2423,7 +2366,6 @@ int pmc_slab_observables(pmc_ctx* c, int with_energy, pmc_stats* out, double* e_
     // two's-complement sums: exact for the signed fields as 64-bit unsigned sums
     uint64_t v[5] = {(uint64_t)st.de_fixed, (uint64_t)st.accepted, (uint64_t)st.trials, (uint64_t)st.evaluated,
                      (uint64_t)ef};
-    if (int rc = exchange_begin(s)) return rc;   // (after the last sweep's exchange on aux2)
     if (s->comm) {
         Rccl& R = rccl();
         if (!R.all_reduce) return fail(PMC_ERR_HIP, "librccl lacks ncclAllReduce");
@@ -2511,18 +2453,21 @@ int pmc_timing_kinds(pmc_ctx* c, int enable, double ms[3], int count[3]) {
             a[c->tkind[k]] += t;
             ++na[c->tkind[k]];
         }
-        // a colour phase split over plane chains: its launches run concurrently, its duration is the
-        // span from the earliest start to the latest stop (times relative to the first start event)
+        // colour phases split over plane chains: the chains' launches run concurrently and a chain starts
+        // its next phase while the others finish theirs, so per-launch times do not add up to the sweep.
+        // The phases' time is the span of each sweep's subsweep launches, from the first start to the
+        // last stop (launch gaps inside the sweep included, shiftCells not), over its 8 phases
         c->span_ms = 0.0;
         c->span_n = 0;
         for (size_t k = 0; k < c->tkind.size(); ++k) {
             if (c->tphase[k] < 0) continue;
+            const int64_t sw = c->tphase[k] / 8;
             bool first = true;
-            for (size_t j = 0; j < k; ++j) first = first && c->tphase[j] != c->tphase[k];
+            for (size_t j = 0; j < k; ++j) first = first && !(c->tphase[j] >= 0 && c->tphase[j] / 8 == sw);
             if (!first) continue;
             float lo = 1e30f, hi = -1e30f;
             for (size_t j = k; j < c->tkind.size(); ++j) {
-                if (c->tphase[j] != c->tphase[k]) continue;
+                if (c->tphase[j] < 0 || c->tphase[j] / 8 != sw) continue;
                 float t0 = 0.0f, t1 = 0.0f;
                 PMC_HIP(hipEventElapsedTime(&t0, c->tev[0], c->tev[2 * j]));
                 PMC_HIP(hipEventElapsedTime(&t1, c->tev[0], c->tev[2 * j + 1]));
@@ -2530,7 +2475,7 @@ int pmc_timing_kinds(pmc_ctx* c, int enable, double ms[3], int count[3]) {
                 hi = t1 > hi ? t1 : hi;
             }
             c->span_ms += hi - lo;
-            ++c->span_n;
+            c->span_n += 8;
         }
     }
     for (int k = 0; k < 3; ++k) {
