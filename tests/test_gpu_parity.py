@@ -644,19 +644,24 @@ def test_bench_rewarm_restores_state(pmc, oracle, slab, rccl):
 @pytest.mark.gpu
 def test_timing_pause_samples_launches(pmc):
     """pmc_timing_pause: launches issued while paused carry no events and are not counted; the
-    collected sums cover exactly the unpaused sweeps (bench.py times every 4th sweep this way)."""
+    collected sums cover exactly the unpaused sweeps (bench.py times every 4th sweep this way).  A
+    sweep is 8 launches per plane chain (pmc_sweep_layout); the phase spans cover 8 phases per timed
+    sweep when there are several chains."""
     ctx = pmc.PmcContext(16)
     ctx.init_lattice(10_000)
+    chains = len(ctx.sweep_layout())
     ctx.timing_kinds(True)
     for s in range(4):
         ctx.timing_pause(s % 2 == 1)
         ctx.sweep(s)
     k = ctx.timing_kinds(False)
-    assert k["n_subsweep"] == 2 * 8 and k["n_shift"] == 2 and k["subsweep_ms"] > 0
+    assert k["n_subsweep"] == 2 * 8 * chains and k["n_shift"] == 2 and k["subsweep_ms"] > 0
+    span, n = ctx.phase_spans()
+    assert (n, span > 0) == ((16, True) if chains > 1 else (0, False))
     ctx.timing_kinds(True)      # a new collection starts unpaused
     ctx.sweep(4)
     k = ctx.timing_kinds(False)
-    assert k["n_subsweep"] == 8 and k["n_shift"] == 1
+    assert k["n_subsweep"] == 8 * chains and k["n_shift"] == 1
 
 
 @pytest.mark.gpu

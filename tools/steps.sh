@@ -9,7 +9,7 @@
 #   mp               tests/test_gpu_multiprocess.py (rank processes over the IPC transport)
 #   smoke            __graft_entry__.smoke()
 #   bench            default bench line (config 3, the driver's --steps 20 --warmup 5)
-#   bench2           config 2
+#   bench2           config 2 (pmc_phase_seq blocks); bench2pc: one pmc_phase call per step
 #   slab1            config 3 through the slab driver, one rank, local halos
 #   bench5           config 5 rehearsal (one 256x256x32 slab, halos through a one-rank RCCL communicator)
 #   emu<R>[-<tp>][-d<us>]   config-4 rehearsal of R ranks (one rank's slab), transport tp (local|ipc|rccl,
@@ -58,6 +58,7 @@ for spec in "$@"; do
         smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $log 2>&1 ;;
         bench) timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $log 2>&1 ;;
         bench2) timeout -k 10 300 python bench.py --config 2 --steps 160 --warmup 8 > $log 2>&1 ;;
+        bench2pc) timeout -k 10 300 python bench.py --config 2 --steps 160 --warmup 8 --phase-calls > $log 2>&1 ;;
         slab1) timeout -k 10 300 python bench.py --slab --no-cpu-baseline --steps 20 --warmup 5 > $log 2>&1 ;;
         bench5) timeout -k 10 300 python bench.py --config 5 --no-cpu-baseline --steps 20 --warmup 5 > $log 2>&1 ;;
         emu*)
@@ -72,7 +73,7 @@ for spec in "$@"; do
                 --rank-timeout 360 > $log 2>&1 ;;
         rocprof) export TMPDIR=/tmp; timeout -k 10 400 rocprofv3 --kernel-trace --stats \
                 -d $OUT/rocprof -o bench -- python3 bench.py --steps 20 --warmup 5 > $log 2>&1 ;;
-        tcc) timeout -k 10 600 bash tools/tcc_traffic.sh $TAG > $log 2>&1 ;;
+        tcc) timeout -k 10 600 bash tools/tcc_traffic.sh ${TAG}_$name > $log 2>&1 ;;
         sq) timeout -k 10 500 bash tools/sq_counters.sh $TAG > $log 2>&1 ;;
         shcnt) timeout -k 10 700 bash tools/shift_counters.sh $TAG > $log 2>&1 ;;
         *) echo "unknown step $step"; exit 2 ;;
