@@ -441,3 +441,28 @@ def test_bench_parity_leg_slab_world4(pmc, oracle):
     assert rec["state_bitwise_equal"] is True
     assert rec["counters_equal"] is True
     assert rec["energy_rel_err"] == 0.0 and rec["acceptance_rel_err"] == 0.0
+
+
+def test_energy_refuses_pending_z_exchange(pmc, oracle):
+    """A z-shift sweep whose halo the next sweep's first run does not read leaves that exchange deferred
+    (PMC_SLAB_DEFER_Z, default on) until the next sweep, pmc_slab_finish or pmc_slab_observables; the energy kernel reads halo neighbours, so
+    pmc_energy refuses the state meanwhile (PMC_ERR_ARG, no silent stale halo and no collective flush
+    inside a local call).  After pmc_slab_finish it equals the oracle's whole-box energy."""
+    from pmc_amd._lib import PmcError
+    from pmc_amd.slab import SlabDriver
+    def deferred(s):   # a z shift whose halo the next sweep's first run does not read (pmc_slab_sweep)
+        _, f, dz = oracle.sweep_plan(1234, s, 2.5)
+        return f == 2 and oracle.sweep_plan(1234, s + 1, 2.5)[0][0] % 2 == (0 if dz > 0 else 1)
+    s_z = next(s for s in range(1, 200) if deferred(s))
+    d = SlabDriver(cps=16, nz_local=16, rank=0, world=1, atoms_total=10_000, transport="local")
+    for s in range(s_z + 1):
+        d.sweep(s)
+    with pytest.raises(PmcError, match="pending"):
+        d.ctx.energy()
+    d.finish()
+    st = oracle.OracleState(oracle.make_params(cps=16))
+    assert st.init_lattice(10_000) == 0
+    assert st.run(0, s_z + 1) == 0
+    assert d.ctx.energy() == pytest.approx(st.energy(), rel=1e-9, abs=1e-9)
+    assert d.ctx.error_flags() == 0
+    d.ctx.close()

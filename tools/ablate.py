@@ -15,8 +15,10 @@ for nm in [int(v) for v in os.environ.get("MOVES", "0,1,5,10,20").split(",")]:
     ctx.init_lattice(atoms)
     # equilibrate a little with the standard chain so the state is not the lattice
     ctx.synchronize()
-    for s in range(2):
-        ctx.sweep(s)
+    for s in range(2):   # one launch per phase (pmc_sweep would split phases over plane chains)
+        for c in range(8):
+            ctx.phase(c, s)
+        ctx.shift(s)
     ctx.synchronize()
     reps = int(os.environ.get("REPS", "5"))
     times = []

@@ -12,10 +12,13 @@ timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU
 python3 - "$OUT" <<'PY'
 import csv, glob, sys, collections
 agg = collections.defaultdict(list)
-for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
-    for r in csv.DictReader(open(f)):
-        if r["Kernel_Name"].split("(")[0].split("<")[0] == "k_subsweep":
-            agg[((f, r["Dispatch_Id"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
+rows = [(f, r) for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True)
+        for r in csv.DictReader(open(f)) if r["Kernel_Name"].split("(")[0].split("<")[0].split("::")[-1] == "k_subsweep"]
+# whole colour phases only: the equilibration sweeps may split phases over plane chains (smaller grids)
+grid = max(int(r["Grid_Size"]) for _, r in rows)
+for f, r in rows:
+    if int(r["Grid_Size"]) == grid:
+        agg[((f, r["Dispatch_Id"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
 per = collections.defaultdict(list)
 for (d, c), v in agg.items():
     per[c].append(sum(v))

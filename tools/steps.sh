@@ -71,7 +71,7 @@ for spec in "$@"; do
                 --no-cpu-baseline --steps 100 --warmup 20 > $log 2>&1 ;;
         mp2bench) timeout -k 10 400 python bench.py --gpus 2 --same-device --config 4 --steps 20 --warmup 5 \
                 --rank-timeout 360 > $log 2>&1 ;;
-        rocprof) export TMPDIR=/tmp; timeout -k 10 400 rocprofv3 --kernel-trace --stats \
+        rocprof) export TMPDIR=/tmp; timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
                 -d $OUT/rocprof -o bench -- python3 bench.py --steps 20 --warmup 5 > $log 2>&1 ;;
         tcc) timeout -k 10 600 bash tools/tcc_traffic.sh ${TAG}_$name > $log 2>&1 ;;
         sq) timeout -k 10 500 bash tools/sq_counters.sh $TAG > $log 2>&1 ;;

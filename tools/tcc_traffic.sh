@@ -20,13 +20,16 @@ python3 - "$OUT" <<'PY'
 import csv, glob, json, sys, collections
 tot = collections.defaultdict(float)
 disp = collections.defaultdict(set)
-for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
-    for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"]
-        if k.startswith("k_subsweep") and "fallback" not in k:
-            tot[r["Counter_Name"]] += float(r["Counter_Value"])
-            disp[r["Counter_Name"]].add((f, r["Dispatch_Id"]))
+rows = [(f, r) for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True)
+        for r in csv.DictReader(open(f)) if "k_subsweep" in r["Kernel_Name"] and "fallback" not in r["Kernel_Name"]]
+# whole colour phases only: the equilibration sweeps may split phases over plane chains (smaller grids)
+grid = max(int(r["Grid_Size"]) for _, r in rows)
+for f, r in rows:
+    if int(r["Grid_Size"]) == grid:
+        tot[r["Counter_Name"]] += float(r["Counter_Value"])
+        disp[r["Counter_Name"]].add((f, r["Dispatch_Id"]))
 per = {c: tot[c] / len(disp[c]) for c in tot}
+per["grid_size"] = grid
 fetch = 2 * per.get("FETCH_SIZE", 0) * 1024          # KiB, doubled (gfx950 correction)
 write = per.get("WRITE_SIZE", 0) * 1024              # KiB
 req = per.get("TCC_EA0_RDREQ_32B", 0) * 32 + per.get("TCC_EA0_RDREQ_64B", 0) * 64 + per.get("TCC_EA0_RDREQ_128B", 0) * 128
