@@ -1408,6 +1408,10 @@ __global__ __launch_bounds__(kWave) void k_sweep_small(DevGeom g, float* __restr
 #define PMC_SHIFT_THREADS 256   // k_shift workgroup size
 #endif
 constexpr int kShiftThreads = PMC_SHIFT_THREADS;
+#ifndef PMC_SHIFT_RUN_LEN
+#define PMC_SHIFT_RUN_LEN 4
+#endif
+constexpr int kShiftRun = PMC_SHIFT_RUN_LEN;   // k_shift_run: cells per lane group along the shift axis
 
 // PMC_SHIFT_NT=1: the output rows as nontemporal stores (streamed past the L2, which then keeps
 // the input rows the neighbour reads re-fetch)
@@ -1570,6 +1574,169 @@ __global__ __launch_bounds__(kShiftThreads) void k_shift(DevGeom g, const float*
             }
         }
         if (live[j] && p == 0) {
+            if constexpr (OFF32)
+                *(int16_t*)((char*)nout + (uint64_t)(c[j] * 2u)) = (int16_t)(nnew > nm ? nm : nnew);
+            else
+                nout[c[j]] = (int16_t)(nnew > nm ? nm : nnew);
+            if (nnew > nm) atomicOr(flags, 1u);
+        }
+    }
+}
+
+// shiftCells along runs of the shift axis (launch_shift_planes; PMC_SHIFT_RUN=0: k_shift).  A lane
+// group (NSLOT lanes, one per slot) takes R cells in a row along f; the dir-neighbour of cell j is
+// cell j+dir of the same run -- already in registers -- except at the run's end, whose neighbour is
+// one extra cell.  Each input cell is then read (R+1)/R times instead of twice (k_shift reads every
+// cell as its own and again as its neighbour's neighbour, 128 B per cell each time), and the keep /
+// take rule is k_shift's (VS shiftCells.h:46-102) cell for cell, so the output is the same bits.
+// Lane groups: x fastest across a wave for f = 1, 2 (four neighbouring cells per wave load), runs
+// along x for f = 0.  Range: local planes [zl0, zl0 + nzr), halo planes included as in k_shift.
+template <int NSLOT, int R, int OFF32>
+__global__ __launch_bounds__(kShiftThreads) void k_shift_run(DevGeom g, const float* __restrict__ din,
+                                                             const int16_t* __restrict__ nin, float* __restrict__ dout,
+                                                             int16_t* __restrict__ nout, int f, float d,
+                                                             uint32_t* __restrict__ flags, int zl0, int nzr) {
+    constexpr int LG = kShiftThreads / NSLOT;   // lane groups per block
+    const int lane = threadIdx.x & (kWave - 1);
+    const int p = threadIdx.x & (NSLOT - 1);
+    const uint32_t G = blockIdx.x * (uint32_t)LG + threadIdx.x / NSLOT;
+    const int nm = g.nmax;
+    const float w = g.w;
+    const int cps_f = f == 0 ? g.cps_x : (f == 1 ? g.cps_y : g.cps_z);
+    const float Lf = f == 0 ? g.Lx : (f == 1 ? g.Ly : g.Lz);
+    const int dir = (d <= 0) ? -1 : 1;                     // VS shiftCells.h:38-44
+    const float s = w * (float)dir;
+    const int len = f == 0 ? g.cps_x : (f == 1 ? g.cps_y : nzr);   // cells along f in the range
+    const uint32_t nruns = (uint32_t)((len + R - 1) / R);
+    // lane group -> (run a, the two other coordinates)
+    uint32_t a;
+    int x = 0, y = 0, zr = 0;                              // zr: plane index within the range
+    if (f == 0) {
+        a = G % nruns;
+        const uint32_t r = G / nruns;
+        y = (int)(r % (uint32_t)g.cps_y);
+        zr = (int)(r / (uint32_t)g.cps_y);
+    } else if (f == 1) {
+        x = (int)(G % (uint32_t)g.cps_x);
+        const uint32_t r = G / (uint32_t)g.cps_x;
+        a = r % nruns;
+        zr = (int)(r / nruns);
+    } else {
+        x = (int)(G % (uint32_t)g.cps_x);
+        const uint32_t r = G / (uint32_t)g.cps_x;
+        y = (int)(r % (uint32_t)g.cps_y);
+        a = r / (uint32_t)g.cps_y;
+    }
+    const bool group_live = f == 2 ? a < nruns : zr < nzr;
+    if (!group_live) a = 0, zr = 0;                        // a valid cell to load from (nothing stored)
+    const int f0 = (int)a * R;
+    const int L = group_live ? (len - f0 < R ? len - f0 : R) : 0;   // live cells of the run
+    const uint32_t plane = (uint32_t)g.cps_x * (uint32_t)g.cps_y;
+    const int pp = p < nm ? p : 0;
+    const int gsh = lane & ~(NSLOT - 1);
+    const unsigned long long gmask = NSLOT == 64 ? ~0ull : ((1ull << (NSLOT & 63)) - 1ull);
+    const unsigned long long below = (1ull << p) - 1ull;
+    // cell j of the run: storage index and coordinate along f (cidf: global, wrapped for halo planes)
+    auto cell_of = [&](int j, int& cidf) -> uint32_t {
+        const int jj = j < L ? j : (L > 0 ? L - 1 : 0);
+        int cx = x, cy = y, cz = zl0 + zr;
+        if (f == 0) cx = f0 + jj; else if (f == 1) cy = f0 + jj; else cz = zl0 + f0 + jj;
+        cidf = f == 0 ? cx : (f == 1 ? cy : g.z0 + cz);
+        if (cidf < 0) cidf += cps_f; else if (cidf >= cps_f) cidf -= cps_f;
+        return (uint32_t)cx + (uint32_t)g.cps_x * (uint32_t)cy + plane * (uint32_t)(cz + g.halo);
+    };
+    auto load3 = [&](uint32_t cell, float (&v)[3]) {
+        if constexpr (OFF32) {
+            const uint32_t o = (cell * (uint32_t)(3 * nm) + (uint32_t)pp * lay_slot()) * 4u;
+            DiskAddr<1>::ld3(din, o, lay_dim(nm), v[0], v[1], v[2]);
+        } else {
+            const uint64_t o = (uint64_t)cell * (uint64_t)(3 * nm) + (uint64_t)pp * lay_slot();
+            v[0] = din[o];
+            v[1] = din[o + lay_dim(nm)];
+            v[2] = din[o + 2 * lay_dim(nm)];
+        }
+    };
+    auto count_of = [&](uint32_t cell) -> int {
+        return OFF32 ? *(const int16_t*)((const char*)nin + (uint64_t)(cell * 2u)) : nin[cell];
+    };
+    uint32_t c[R];
+    int cid[R], ncur[R];
+    float own[R][3];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        c[j] = cell_of(j, cid[j]);
+        const int n0 = count_of(c[j]);
+        ncur[j] = j < L ? n0 : 0;
+        load3(c[j], own[j]);
+    }
+    // the extra cell: the dir-neighbour of the run's edge cell (its last live cell for dir > 0, its
+    // first for dir < 0)
+    const int je = dir > 0 ? (L > 0 ? L - 1 : 0) : 0;
+    int cide;
+    const uint32_t ce = cell_of(je, cide);
+    int nbe = cide + dir;
+    if (nbe < 0) nbe = cps_f - 1; else if (nbe >= cps_f) nbe = 0;
+    uint32_t cx = ce;   // storage index of the extra cell
+    {
+        const int zl = (int)(ce / plane) - g.halo;
+        const uint32_t rem = ce - (uint32_t)(zl + g.halo) * plane;
+        int ex = (int)(rem % (uint32_t)g.cps_x), ey = (int)(rem / (uint32_t)g.cps_x), ez = zl;
+        if (f == 0) ex = nbe; else if (f == 1) ey = nbe; else ez = g.halo ? zl + dir : nbe;
+        cx = (uint32_t)ex + (uint32_t)g.cps_x * (uint32_t)ey + plane * (uint32_t)(ez + g.halo);
+    }
+    const int nne0 = count_of(cx);
+    const int nne = L > 0 ? nne0 : 0;
+    float ext[3];
+    load3(cx, ext);
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        // the dir-neighbour: cell j + dir of the run when that is a live cell, else the extra one
+        const int jn = j + dir;
+        const bool in_run = jn >= 0 && jn < L;
+        const int jl = j + 1 < R ? j + 1 : R - 1, jr = j > 0 ? j - 1 : 0;   // compile-time candidates
+        float nbv[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) nbv[k] = in_run ? (dir > 0 ? own[jl][k] : own[jr][k]) : ext[k];
+        const int nnb = in_run ? (dir > 0 ? ncur[jl] : ncur[jr]) : nne;
+        int nbg = cid[j] + dir;
+        if (nbg < 0) nbg = cps_f - 1; else if (nbg >= cps_f) nbg = 0;
+        const float offset = (float)cid[j] * w - Lf / 2.0f;          // VS :46
+        const float offset_nb = (float)nbg * w - Lf / 2.0f;
+        const float xf = f == 0 ? own[j][0] : (f == 1 ? own[j][1] : own[j][2]);
+        const float xfn = f == 0 ? nbv[0] : (f == 1 ? nbv[1] : nbv[2]);
+        const float D = (xf - offset) - d;               // shortDisk - d
+        const float Dn = (xfn - offset_nb) - d;
+        const bool keep = (p < ncur[j]) && (D > 0 && D <= w);
+        const bool take = (j < L) && (p < nnb) && !(Dn > 0 && Dn <= w);
+        const unsigned long long km = (__ballot(keep) >> gsh) & gmask;
+        const unsigned long long tm = (__ballot(take) >> gsh) & gmask;
+        const int nk = __popcll(km);
+        const int nnew = nk + __popcll(tm);
+        auto out_at = [&](int dst) -> float* {
+            const uint32_t e = (uint32_t)dst * lay_slot();
+            if constexpr (OFF32)
+                return (float*)((char*)dout + (uint64_t)((c[j] * (uint32_t)(3 * nm) + e) * 4u));
+            else
+                return dout + (uint64_t)c[j] * (uint64_t)(3 * nm) + (uint64_t)e;
+        };
+        if (keep) {
+            const int dst = __popcll(km & below);
+            if (dst < nm) {
+                float* q = out_at(dst);
+#pragma unroll
+                for (int dim = 0; dim < 3; ++dim) shift_store(q + dim * lay_dim(nm), (dim == f) ? D + offset : own[j][dim]);
+            }
+        }
+        if (take) {
+            const int dst = nk + __popcll(tm & below);
+            if (dst < nm) {
+                float* q = out_at(dst);
+#pragma unroll
+                for (int dim = 0; dim < 3; ++dim)   // own offset (VS shiftCells.h:96)
+                    shift_store(q + dim * lay_dim(nm), (dim == f) ? ((Dn + offset) + s) : nbv[dim]);
+            }
+        }
+        if (j < L && p == 0) {
             if constexpr (OFF32)
                 *(int16_t*)((char*)nout + (uint64_t)(c[j] * 2u)) = (int16_t)(nnew > nm ? nm : nnew);
             else
@@ -2866,8 +3033,21 @@ hipError_t launch_shift_planes(const DevGeom& g, const float* din, const int16_t
     static const bool off32_env = env_cells("PMC_SHIFT_OFF32", 1) != 0;
     const int64_t bytes = (int64_t)g.cps_x * g.cps_y * (g.nz_local + 2 * g.halo) * 3 * g.nmax * 4;
     const bool off32 = off32_env && bytes < ((int64_t)1 << 32);
+    // PMC_SHIFT_RUN (default 1): runs of kShiftRun cells along the shift axis per lane group (k_shift_run)
+    static const bool run_env = env_cells("PMC_SHIFT_RUN", 1) != 0;
+    const int nzr = zl_end - zl_begin;
+    const int len = f == 0 ? g.cps_x : (f == 1 ? g.cps_y : nzr);
+    const int64_t runs = (int64_t)((len + kShiftRun - 1) / kShiftRun) *
+                         (f == 0 ? (int64_t)g.cps_y * nzr : (f == 1 ? (int64_t)g.cps_x * nzr : (int64_t)g.cps_x * g.cps_y));
+    const int64_t lgs = kShiftThreads / g.nslot;
+    const dim3 rgrid((unsigned)((runs + lgs - 1) / lgs));
     auto go = [&](auto ns) {
         constexpr int NS = decltype(ns)::value;
+        if (run_env) {
+            if (off32) launch_k(k_shift_run<NS, kShiftRun, 1>, rgrid, block, 0, st, tm, g, din, nin, dout, nout, f, d, flags, z0, nzr);
+            else launch_k(k_shift_run<NS, kShiftRun, 0>, rgrid, block, 0, st, tm, g, din, nin, dout, nout, f, d, flags, z0, nzr);
+            return;
+        }
         if (off32) launch_k(k_shift<NS, U, 1>, grid, block, 0, st, tm, g, din, nin, dout, nout, f, d, flags, z0);
         else launch_k(k_shift<NS, U, 0>, grid, block, 0, st, tm, g, din, nin, dout, nout, f, d, flags, z0);
     };

@@ -117,15 +117,17 @@ def test_shift_parity(pmc, oracle, f, d):
     assert int(got_n.sum()) == 10_000
 
 
-@pytest.mark.parametrize("cps,atoms", [(6, 600), (12, 5000), (20, 30000)])
-@pytest.mark.parametrize("f,d", [(0, 0.9), (1, -0.6), (2, 1.1), (2, -1.2)])
+@pytest.mark.parametrize("cps,atoms", [(6, 600), (12, 5000), (20, 30000), ((10, 6, 14), 2500)])
+@pytest.mark.parametrize("f,d", [(0, 0.9), (1, -0.6), (2, 1.1), (2, -1.2), (0, -0.8), (1, 0.5)])
 def test_shift_sizes_parity(pmc, oracle, cps, atoms, f, d):
-    """shiftCells at other box sizes (6, 12, 20 cells per side) along every axis, both directions."""
-    ctx = _ctx(pmc, cps)
+    """shiftCells at other box sizes (6, 12, 20 cells per side; 10 x 6 x 14) along every axis, both
+    directions: k_shift_run's runs of 4 cells along the shift axis end short (6, 10, 14) or exactly."""
+    cx, cy, cz = cps if isinstance(cps, tuple) else (cps, cps, cps)
+    ctx = _ctx(pmc, cx, cps_y=cy, cps_z=cz)
     ctx.init_lattice(atoms)
     ctx.start(0, 1)
     disk, n = ctx.copy_out()
-    st = _ostate(oracle, cps)
+    st = _ostate(oracle, cx, cps_y=cy, cps_z=cz)
     st.disk[:] = disk
     st.n[:] = n
     import torch

@@ -19,7 +19,7 @@ per = collections.defaultdict(dict)
 for f in glob.glob(f"{root}/p*/**/*counter_collection.csv", recursive=True):
     vals = collections.defaultdict(float)
     for r in csv.DictReader(open(f)):
-        if "k_shift<" in r["Kernel_Name"]:
+        if "k_shift<" in r["Kernel_Name"] or "k_shift_run<" in r["Kernel_Name"]:
             vals[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
     for (d, c), v in vals.items():
         per[c].setdefault(f, []).append(v)
