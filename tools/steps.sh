@@ -16,6 +16,8 @@
 #                    default local), injected exchange delay us
 #   mp2bench         bench.py --gpus 2 --same-device --config 4 (rank processes, IPC)
 #   rocprof          rocprofv3 --kernel-trace --stats of the default bench command
+#   trace8           rocprofv3 kernel trace of the 8-rank IPC rehearsal + tools/timeline_stats.py
+#   py:<file>        python tools/<file> (analysis scripts, e.g. stamps.py with PMC_LIB_PATH=...@py:stamps.py)
 #   tcc | sq | shcnt  counter passes: k_subsweep traffic (tools/tcc_traffic.sh), its SQ instruction mix
 #                    (tools/sq_counters.sh), k_shift traffic + wave states (tools/shift_counters.sh)
 # A step may carry environment variables: PMC_QUAD_CELLS=40000@bench2 (A/B switches).
@@ -73,6 +75,10 @@ for spec in "$@"; do
                 --rank-timeout 360 > $log 2>&1 ;;
         rocprof) export TMPDIR=/tmp; timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
                 -d $OUT/rocprof -o bench -- python3 bench.py --steps 20 --warmup 5 > $log 2>&1 ;;
+        py:*) timeout -k 10 300 python tools/${step#py:} > $log 2>&1 ;;
+        trace8) export TMPDIR=/tmp; timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace8 -o run \
+                -- python3 bench.py --config 4 --emulate-ranks 8 --transport ipc --no-cpu-baseline --steps 40 --warmup 10 \
+                > $log 2>&1 && python3 tools/timeline_stats.py $OUT/trace8/run_kernel_trace.csv 20 > $OUT/trace8_timeline.txt 2>&1 ;;
         tcc) timeout -k 10 600 bash tools/tcc_traffic.sh ${TAG}_$name > $log 2>&1 ;;
         sq) timeout -k 10 500 bash tools/sq_counters.sh $TAG > $log 2>&1 ;;
         shcnt) timeout -k 10 700 bash tools/shift_counters.sh $TAG > $log 2>&1 ;;
@@ -83,6 +89,8 @@ for spec in "$@"; do
     if [ $rc -ne 0 ]; then echo "step $spec failed rc $rc"; tail -40 $log; exit $rc; fi
     case $step in
         tests*|mp|smoke) tail -1 $log ;;
+        py:*) tail -25 $log ;;
+        trace8) cat $OUT/trace8_timeline.txt | head -40 ;;
         tcc|sq|shcnt) tail -12 $log ;;
         rocprof) python3 tools/rocprof_timed_mean.py $OUT/rocprof 2>&1 | tail -8 ;;
         *) grep '^{' $log > $OUT/$name.json; summ $OUT/$name.json ;;
