@@ -138,11 +138,11 @@ def host_cpu() -> dict:
 
 
 def cpu_baseline(disk, n, cps: int, sweep0: int, serial_planes: int, cps_z: int = 0,
-                 phase: tuple[int, int] | None = None) -> tuple[dict, object]:
+                 phase: tuple[int, int] | None = None, sweeps: int = 1) -> tuple[dict, object]:
     """The C oracle (the reference has no CPU path: SURVEY.md 0/8c) timed on this host:
     (i) serial, one core: one colour phase over planes [0, serial_planes);
     (ii) OpenMP over the cells of a colour on the cores of one socket (one thread per physical
-    core, limited by the CPUs/cgroup quota this process may use): one full sweep from the GPU
+    core, limited by the CPUs/cgroup quota this process may use): `sweeps` full sweeps from the GPU
     state, or with phase = (colour, sweep index) that one colour phase of the whole box (config 2).
     Returns the JSON object and the oracle state after (ii) for the parity leg."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -180,13 +180,14 @@ def cpu_baseline(disk, n, cps: int, sweep0: int, serial_planes: int, cps_z: int 
     if phase:
         st.subsweep(pmc_oracle.colour_offset(phase[0]), phase[1])
     else:
-        st.run(sweep0, 1)
+        st.run(sweep0, sweeps)
     dt = time.perf_counter() - t0
     par = st.stats.trials / dt
     cores_socket = host["cores_per_socket"] or threads
-    what = (f"colour phase {phase[0]} (sweep index {phase[1]})" if phase else "full sweep")
+    what = (f"one colour phase {phase[0]} (sweep index {phase[1]})" if phase else
+            ("one full sweep" if sweeps == 1 else f"{sweeps} full sweeps"))
     out = {"value": par, "unit": "trial-moves/s", "cores": threads, "kind": "port",
-           "sample": f"one {what} of the {box} box from the GPU state, C oracle, OpenMP over the cells "
+           "sample": f"{what} of the {box} box from the GPU state, C oracle, OpenMP over the cells "
                      f"of a colour on {threads} threads (one per physical core of socket 0; limited by "
                      f"{limited_by}), {dt:.2f} s",
            "serial": {"value": serial, "cores": 1,
@@ -439,6 +440,9 @@ def main() -> int:
                     help="planes of the serial CPU sample's colour phase (default: the whole box up to 128)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--graph", action="store_true", help="replay the timed sweeps as one hipGraph")
+    ap.add_argument("--cpu-sweeps", type=int, default=3,
+                    help="whole-box CPU baseline: full sweeps the OpenMP oracle times (and the parity leg reruns "
+                         "on the GPU from the same state)")
     ap.add_argument("--no-events", action="store_true",
                     help="no per-launch HIP events in the timed region (no roofline; overhead check)")
     ap.add_argument("--rewarm", type=int, default=12,
@@ -757,8 +761,9 @@ def main() -> int:
             if rank == 0:
                 try:
                     ph = (first % 8, first // 8) if config == "2" else None
-                    cpu, ost = cpu_baseline(disk_h, n_h, cps, first, sp, phase=ph)
-                    parity = parity_leg(sim, one_sweep, disk_h, n_h, first, 1, e_start, ost)
+                    cs = 1 if ph else max(1, args.cpu_sweeps)
+                    cpu, ost = cpu_baseline(disk_h, n_h, cps, first, sp, phase=ph, sweeps=cs)
+                    parity = parity_leg(sim, one_sweep, disk_h, n_h, first, cs, e_start, ost)
                     if config == "2":
                         parity["sweeps"] = 0
                         parity["phase"] = {"colour": first % 8, "sweep_index": first // 8}
