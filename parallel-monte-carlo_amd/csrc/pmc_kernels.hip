@@ -28,9 +28,6 @@
 
 namespace pmc {
 
-#ifndef PMC_SHIFT_XCD
-#define PMC_SHIFT_XCD 0   // shiftCells blocks in XCD-contiguous order (A/B)
-#endif
 #ifndef PMC_MOVE_PRIO
 #define PMC_MOVE_PRIO 2    // wave priority of the moves (their serial tail one above); 0: no s_setprio
 #endif
@@ -1439,40 +1436,9 @@ __global__ __launch_bounds__(kShiftThreads) void k_shift(DevGeom g, const float*
     constexpr int CPB = kShiftThreads / NSLOT;
     const int lane = threadIdx.x & (kWave - 1);
     const int p = threadIdx.x & (NSLOT - 1);
-#if PMC_SHIFT_XCD
-    // 1-D grid in XCD-contiguous order: block b runs on XCD b % 8, so XCD k takes rows
-    // [k*R/8, (k+1)*R/8) of the (x-block, y, plane) order and the neighbour rows a shift along y or
-    // z reads are mostly ones its own L2 just fetched (speed only)
-    const uint32_t gx = (uint32_t)((g.cps_x + CPB * U - 1) / (CPB * U));
-    uint32_t lb = blockIdx.x;
-    const uint32_t nblk = gridDim.x;
-    if ((nblk & 7u) == 0u) lb = (lb & 7u) * (nblk >> 3) + (lb >> 3);
-    const uint32_t rowid = lb / gx;
-    const int bx = (int)(lb - rowid * gx);
-    const int y = (int)(rowid % (uint32_t)g.cps_y), zl = zl0 + (int)(rowid / (uint32_t)g.cps_y);
-#else
-    int bx, y, zl;
-    if (gridDim.y == 1 && gridDim.z == 1) {
-        // y-chunked XCD order (1-D grid, launch_shift_planes when cps_y % 8 == 0): block b runs on
-        // XCD b % 8 (round-robin dispatch), and XCD k takes the rows [k*R, (k+1)*R) (R = cps_y/8)
-        // of every plane, x-blocks fastest, then the rows of the chunk, then the planes.  A shift
-        // along y reads the neighbour row y+dir, along z the same row of plane z+dir: both lie on
-        // the same XCD except at the chunk borders, so their lines come from that XCD's L2 (the
-        // plain 3-D grid puts consecutive rows on different XCDs).  Speed only.
-        const uint32_t gx = (uint32_t)((g.cps_x + CPB * U - 1) / (CPB * U));
-        const uint32_t R = (uint32_t)g.cps_y >> 3;
-        const uint32_t b = blockIdx.x, k = b & 7u, i = b >> 3;
-        const uint32_t t = i / gx;
-        bx = (int)(i - t * gx);
-        const uint32_t zz = t / R;
-        y = (int)(k * R + (t - zz * R));
-        zl = zl0 + (int)zz;
-    } else {
-        bx = (int)blockIdx.x;
-        y = (int)blockIdx.y;
-        zl = zl0 + (int)blockIdx.z;
-    }
-#endif
+    // (the XCD-contiguous and y-chunked block orders measured no faster, profiles/r03o_shift_xcd_ab.txt,
+    // r04 DESIGN section 6; removed in round 5)
+    const int bx = (int)blockIdx.x, y = (int)blockIdx.y, zl = zl0 + (int)blockIdx.z;
     const int nm = g.nmax;
     const float w = g.w;
     const int cps_f = f == 0 ? g.cps_x : (f == 1 ? g.cps_y : g.cps_z);
@@ -3013,18 +2979,9 @@ hipError_t launch_shift_planes(const DevGeom& g, const float* din, const int16_t
 #endif
     constexpr int U = PMC_SHIFT_U;   // cells per lane group, loads hoisted
     const int cpb = kShiftThreads / g.nslot;
-#if PMC_SHIFT_XCD
-    dim3 grid((unsigned)(((g.cps_x + cpb * U - 1) / (cpb * U)) * g.cps_y * (zl_end - zl_begin))), block(kShiftThreads);
-#else
-    // PMC_SHIFT_YCHUNK=1 (and cps_y % 8 == 0): the 1-D y-chunked XCD order (k_shift)
-    static const bool ychunk = env_cells("PMC_SHIFT_YCHUNK", 0) == 1;
     const unsigned gxs = (unsigned)((g.cps_x + cpb * U - 1) / (cpb * U));
-    // (the 3-D grid has gridDim.y = cps_y >= 4, so k_shift tells the two forms apart)
-    const dim3 grid = (ychunk && g.cps_y % 8 == 0)
-                          ? dim3(gxs * (unsigned)g.cps_y * (unsigned)(zl_end - zl_begin))
-                          : dim3(gxs, (unsigned)g.cps_y, (unsigned)(zl_end - zl_begin));
+    const dim3 grid(gxs, (unsigned)g.cps_y, (unsigned)(zl_end - zl_begin));
     const dim3 block(kShiftThreads);
-#endif
     const int z0 = zl_begin;
     // 32-bit byte offsets when the storage is below 4 GiB (PMC_SHIFT_OFF32=0: the 64-bit form).  With
     // the reference rows it measured no faster (0.203-0.204 against 0.199-0.203 ms,

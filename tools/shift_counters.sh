@@ -24,7 +24,7 @@ for f in glob.glob(f"{root}/p*/**/*counter_collection.csv", recursive=True):
     for (d, c), v in vals.items():
         per[c].setdefault(f, []).append(v)
 mean = {c: sum(sum(v) for v in fs.values()) / sum(len(v) for v in fs.values()) for c, fs in per.items()}
-out = {"kernel": "k_shift<16,8> (shiftCells, 128^3 / 1e7)", "counters_per_launch": mean}
+out = {"kernel": "k_shift_run<16,4> (shiftCells, 128^3 / 1e7; k_shift<16,8> with PMC_SHIFT_RUN=0)", "counters_per_launch": mean}
 if "FETCH_SIZE" in mean:
     out["read_bytes_per_launch"] = 2 * mean["FETCH_SIZE"] * 1024
 if "WRITE_SIZE" in mean:
