@@ -735,7 +735,10 @@ def main() -> int:
                 "launch_ms": avg_launch_s * 1e3 if avg_launch_s else None,
                 "launches_timed": n_launch,
                 **({"phase_ms": phase_s * 1e3, "phases_timed": span_n,
-                    "algorithmic_bytes_per_phase": phase_bytes} if phase_s else {}),
+                    "algorithmic_bytes_per_phase": phase_bytes,
+                    # the per-launch view rocprofv3's kernel statistics give (half-box launches, two at once)
+                    "launch_achieved": sub_launch_bytes / avg_launch_s / 1e9 if avg_launch_s else None}
+                   if phase_s else {}),
                 "shift_ms": tm["shift_ms"] / tm["n_shift"] if tm["n_shift"] else None,
                 "shift": ({"algorithmic_bytes_per_launch": shift_bytes,
                            "achieved": shift_bytes / (tm["shift_ms"] / tm["n_shift"] * 1e-3) / 1e9,
