@@ -1,4 +1,4 @@
-"""Summarise A/B bench lines (tools/r04_strong_ab.sh, r04_variants_ab.sh, r04_env_ab.sh outputs:
+"""Summarise A/B bench lines (tools/archive/r04_strong_ab.sh, r04_variants_ab.sh, r04_env_ab.sh outputs:
 <variant>[_d<delay>_R<ranks>]_<rep>.json) as one table row per file, grouped by variant.
 
   python tools/ab_summary.py gpurun_out/r04c_ab [...] > profiles/r04_strong_variants.txt

@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU box: the whole GPU test suite, the default bench line, the strong-scaling rehearsal at 8 and 4
-# ranks, and the energy timing.  Usage: bash tools/r02_check.sh <tag>
+# ranks, and the energy timing.  Usage: bash tools/archive/r02_check.sh <tag>
 set -o pipefail
 O=gpurun_out/$1; mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 150 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-2 measurement set on the GPU box: default bench line, eager vs hipGraph A/B, occupancy
 # probes, rocprofv3 kernel-trace stats of the bench, SQ instruction counters and the k_subsweep
-# traffic passes.  Usage: bash tools/r02_profile.sh <tag>
+# traffic passes.  Usage: bash tools/archive/r02_profile.sh <tag>
 set -o pipefail
 T=$1; O=gpurun_out/$T; mkdir -p $O
 export TMPDIR=/tmp

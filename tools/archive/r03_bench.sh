@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 3 bench lines: config 3 (driver command), config 4 slab at one rank and as an 8-rank
 # rehearsal, config 5 rehearsal -- each with CPU baseline and parity leg.
-# Usage (GPU box, repo root): bash tools/r03_bench.sh <tag>
+# Usage (GPU box, repo root): bash tools/archive/r03_bench.sh <tag>
 set -o pipefail
 O=gpurun_out/$1; mkdir -p $O
 run() { local n=$1; shift; timeout -k 10 400 python bench.py "$@" > $O/$n.log 2>&1 || { tail -30 $O/$n.log; exit 1; }

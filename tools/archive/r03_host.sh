@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 3: strong-scaling rehearsal at 8 ranks with the host restricted to 2 CPUs (an 8-GPU node's
-# 16-CPU quota / 8 ranks) against the unrestricted one, alternating.  Usage: bash tools/r03_host.sh <tag>
+# 16-CPU quota / 8 ranks) against the unrestricted one, alternating.  Usage: bash tools/archive/r03_host.sh <tag>
 set -o pipefail
 O=gpurun_out/$1; mkdir -p $O
 for i in 1 2; do

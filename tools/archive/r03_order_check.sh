@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 3: the create-ordering test against the round-2 library (expected to expose the race) and
-# the current one, then the whole GPU suite.  Usage (GPU box, repo root): bash tools/r03_order_check.sh <tag>
+# the current one, then the whole GPU suite.  Usage (GPU box, repo root): bash tools/archive/r03_order_check.sh <tag>
 set -o pipefail
 O=gpurun_out/$1; mkdir -p $O
 T="python -u -m pytest tests/test_gpu_parity.py -k busy_null_stream -v --timeout 120 --timeout-method thread"

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 3: the whole GPU suite (with a heartbeat file: the config-5 oracle test is quiet for ~1 min)
-# Usage (GPU box, repo root): bash tools/r03_tests.sh <tag> [pytest args]
+# Usage (GPU box, repo root): bash tools/archive/r03_tests.sh <tag> [pytest args]
 set -o pipefail
 O=gpurun_out/$1; shift; mkdir -p $O
 ( while sleep 20; do date +%T >> $O/heartbeat; done ) & HB=$!

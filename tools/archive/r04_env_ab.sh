@@ -1,6 +1,6 @@
 #!/bin/bash
 # Config-3 (or CONFIG) bench A/B over named environment variants of the same build, alternating,
-# REPS rounds.  Usage: bash tools/r04_env_ab.sh <tag> "name:VAR=v,VAR=v" ...
+# REPS rounds.  Usage: bash tools/archive/r04_env_ab.sh <tag> "name:VAR=v,VAR=v" ...
 set -o pipefail
 T=$1; shift
 O=gpurun_out/$T; mkdir -p $O

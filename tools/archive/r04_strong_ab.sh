@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 4: strong-scaling rehearsal A/B over interior chain count and injected exchange delay.
 # bench.py --config 4 --emulate-ranks R (one rank's slab of the 128^3/1e7 box, product C slab driver),
-# alternating variants, REPS rounds.  Usage: R=8 CHAINS="2 3" DELAYS="0 80" REPS="1 2 3" bash tools/r04_strong_ab.sh <tag>
+# alternating variants, REPS rounds.  Usage: R=8 CHAINS="2 3" DELAYS="0 80" REPS="1 2 3" bash tools/archive/r04_strong_ab.sh <tag>
 set -o pipefail
 T=${1:-r04_strong}
 O=gpurun_out/$T; mkdir -p $O

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Strong-scaling rehearsal A/B over named environment variants of the product library (same build):
 # bench.py --config 4 --emulate-ranks R, alternating variants x injected delays, REPS rounds.
-# Usage: R=8 DELAYS="0 80" REPS="1 2" bash tools/r04_variants_ab.sh <tag> "name:VAR=v,VAR=v" ...
+# Usage: R=8 DELAYS="0 80" REPS="1 2" bash tools/archive/r04_variants_ab.sh <tag> "name:VAR=v,VAR=v" ...
 set -o pipefail
 T=$1; shift
 O=gpurun_out/$T; mkdir -p $O

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-2 final measurement set (GPU box): GPU tests, the driver's bench command, rocprofv3 kernel
 # stats of the same command, config 5 / 5box lines, strong rehearsal 8/4, energy timing.
-# Usage: bash tools/s2_profile.sh <tag>
+# Usage: bash tools/archive/s2_profile.sh <tag>
 set -o pipefail
 T=$1; O=gpurun_out/$T; mkdir -p $O
 export TMPDIR=/tmp
