@@ -2828,6 +2828,17 @@ static void launch_subsweep_n(const DevGeom& g, float* disk, const int16_t* n, i
     else launch_subsweep_t<64, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st, tm);
 }
 
+// a timed launch with nothing to visit (a chain whose planes hold no plane of the colour): its
+// events are recorded anyway (zero duration), so the caller's timing entry stays valid
+static hipError_t skip_launch(hipStream_t st, const LaunchTiming* tm) {
+    if (tm && tm->start) {
+        hipError_t e = hipEventRecord(tm->start, st);
+        if (e == hipSuccess) e = hipEventRecord(tm->stop, st);
+        return e;
+    }
+    return hipSuccess;
+}
+
 hipError_t launch_subsweep_boundary(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
                                     uint32_t sweep, unsigned long long* stats, int* ovf, int zl_begin, int zl_end,
                                     float* mirror, int mirror_mode, hipStream_t st, const LaunchTiming* tm) {
@@ -2835,7 +2846,7 @@ hipError_t launch_subsweep_boundary(const DevGeom& g, float* disk, const int16_t
     const int nczc = g.nz_local / 2;
     int cz0 = ceil_half(zl_begin - oz), cz1 = ceil_half(zl_end - oz);
     if (cz1 > nczc) cz1 = nczc;
-    if (cz1 <= cz0) return hipSuccess;
+    if (cz1 <= cz0) return skip_launch(st, tm);
     const int64_t bytes = (int64_t)g.cps_x * g.cps_y * (g.nz_local + 2 * g.halo) * 3 * g.nmax * 4;
     if (bytes < ((int64_t)1 << 32)) launch_direct_n<true>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, cz1 - cz0, mirror, mirror_mode, st, tm);
     else launch_direct_n<false>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, cz1 - cz0, mirror, mirror_mode, st, tm);
@@ -2907,7 +2918,7 @@ hipError_t launch_subsweep(const DevGeom& g, float* disk, const int16_t* n, int 
     const int nczc = g.nz_local / 2;
     int cz0 = ceil_half(zl_begin - oz), cz1 = ceil_half(zl_end - oz);
     if (cz1 > nczc) cz1 = nczc;
-    if (cz1 <= cz0) return hipSuccess;
+    if (cz1 <= cz0) return skip_launch(st, tm);
     const int ncz = cz1 - cz0;
     // 32-bit byte offsets when the disk buffer is below 4 GiB (every single-GPU 256^3 config)
     // (test hook: PMC_FORCE_ADDR64 takes the 64-bit path for any size)

@@ -108,12 +108,14 @@ def test_ipc_processes_equal_oracle(pmc, oracle, tmp_path, world, cps, cps_z, at
     assert tot == whole     # (a restart restores the snapshot's counters: the same totals)
 
 
-def test_bench_two_rank_processes_same_device(pmc):
-    """bench.py --gpus 2 launches two rank processes itself; with --same-device both use GPU 0 and the
-    halos go through the IPC transport.  The N > 1 line carries the gathered whole-box parity leg."""
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_rank_processes_same_device(pmc, world):
+    """bench.py --gpus N launches N rank processes itself; with --same-device all use GPU 0 and the
+    halos go through the IPC transport (world 8: 4 planes per rank of the 32^3 box).  The N > 1 line
+    carries the gathered whole-box parity leg."""
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
     env["PMC_IPC_TIMEOUT_S"] = "30"
-    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--same-device", "--config", "4",
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(world), "--same-device", "--config", "4",
                         "--cps", "32", "--atoms", "120000", "--steps", "4", "--warmup", "2", "--rewarm", "2",
                         "--serial-planes", "4", "--rank-timeout", "240"],
                        env=env, capture_output=True, text=True, timeout=300)
@@ -121,7 +123,7 @@ def test_bench_two_rank_processes_same_device(pmc):
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2
+    assert d["n_gpus"] == world
     assert "IPC" in d["config"]["parallelism"], d["config"]["parallelism"]
     assert d["error_flags"] == 0
     par = d["parity"]

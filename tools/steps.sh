@@ -15,7 +15,7 @@
 #   bench5           config 5 rehearsal (one 256x256x32 slab, halos through a one-rank RCCL communicator)
 #   emu<R>[-<tp>][-d<us>]   config-4 rehearsal of R ranks (one rank's slab), transport tp (local|ipc|rccl,
 #                    default local), injected exchange delay us
-#   mp2bench         bench.py --gpus 2 --same-device --config 4 (rank processes, IPC)
+#   mp2bench         bench.py --gpus 2 --same-device --config 4 (rank processes, IPC); mp4bench, mp8bench: 4, 8
 #   rocprof          rocprofv3 --kernel-trace --stats of the default bench command
 #   trace8           rocprofv3 kernel trace of the 8-rank IPC rehearsal + tools/timeline_stats.py
 #   py:<file>        python tools/<file> (analysis scripts, e.g. stamps.py with PMC_LIB_PATH=...@py:stamps.py)
@@ -75,6 +75,8 @@ for spec in "$@"; do
                 --no-cpu-baseline --steps 100 --warmup 20 > $log 2>&1 ;;
         mp2bench) timeout -k 10 400 python bench.py --gpus 2 --same-device --config 4 --steps 20 --warmup 5 \
                 --rank-timeout 360 > $log 2>&1 ;;
+        mp4bench|mp8bench) R=${step:2:1}; timeout -k 10 500 python bench.py --gpus $R --same-device --config 4 --steps 10 \
+                --warmup 3 --rank-timeout 460 > $log 2>&1 ;;
         rocprof) export TMPDIR=/tmp; timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
                 -d $OUT/rocprof -o bench -- python3 bench.py --steps 20 --warmup 5 > $log 2>&1 ;;
         py:*) timeout -k 10 300 python tools/${step#py:} > $log 2>&1 ;;
