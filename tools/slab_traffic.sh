@@ -16,7 +16,7 @@ for shape in "4:16:--config 4 --emulate-ranks 8" "4:32:--config 4 --emulate-rank
   echo "$key done"
 done
 python3 - "$O" <<'PY'
-import csv, glob, json, os, sys, collections
+import csv, glob, json, os, re, sys, collections
 root = sys.argv[1]
 out = {}
 for d in sorted(glob.glob(root + "/*_*/")):
@@ -26,8 +26,8 @@ for d in sorted(glob.glob(root + "/*_*/")):
         vals = collections.defaultdict(float)
         for f in glob.glob(f"{d}/{c}/**/*counter_collection.csv", recursive=True):
             for r in csv.DictReader(open(f)):
-                k = r["Kernel_Name"].split("(")[0].split("<")[0].split()[-1]
-                if k == "k_subsweep" and r["Counter_Name"] == c:
+                m = re.search(r"(k_\w+)", r["Kernel_Name"])
+                if m and m.group(1) == "k_subsweep" and r["Counter_Name"] == c:
                     vals[(f, r["Dispatch_Id"])] += float(r["Counter_Value"])
         per[c] = (sum(vals.values()) / len(vals), len(vals)) if vals else (None, 0)
     rd = 2 * per["FETCH_SIZE"][0] * 1024 if per["FETCH_SIZE"][0] is not None else None

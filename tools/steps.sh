@@ -19,8 +19,9 @@
 #   rocprof          rocprofv3 --kernel-trace --stats of the default bench command
 #   trace8           rocprofv3 kernel trace of the 8-rank IPC rehearsal + tools/timeline_stats.py
 #   py:<file>        python tools/<file> (analysis scripts, e.g. stamps.py with PMC_LIB_PATH=...@py:stamps.py)
-#   tcc | sq | shcnt  counter passes: k_subsweep traffic (tools/tcc_traffic.sh), its SQ instruction mix
-#                    (tools/sq_counters.sh), k_shift traffic + wave states (tools/shift_counters.sh)
+#   tcc | sq | shcnt | slabtcc  counter passes: k_subsweep traffic (tools/tcc_traffic.sh), its SQ
+#                    instruction mix (tools/sq_counters.sh), shiftCells traffic + wave states
+#                    (tools/shift_counters.sh), the slab interior launches' traffic (tools/slab_traffic.sh)
 # A step may carry environment variables: PMC_QUAD_CELLS=40000@bench2 (A/B switches).
 set -o pipefail
 TAG=${1:?tag}; shift
@@ -86,6 +87,7 @@ for spec in "$@"; do
         tcc) timeout -k 10 600 bash tools/tcc_traffic.sh ${TAG}_$name > $log 2>&1 ;;
         sq) timeout -k 10 500 bash tools/sq_counters.sh $TAG > $log 2>&1 ;;
         shcnt) timeout -k 10 700 bash tools/shift_counters.sh $TAG > $log 2>&1 ;;
+        slabtcc) timeout -k 10 900 bash tools/slab_traffic.sh $TAG > $log 2>&1 ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
     rc=$?
@@ -95,7 +97,7 @@ for spec in "$@"; do
         tests*|mp|smoke) tail -1 $log ;;
         py:*) tail -25 $log ;;
         trace8) cat $OUT/trace8_timeline.txt | head -40 ;;
-        tcc|sq|shcnt) tail -12 $log ;;
+        tcc|sq|shcnt|slabtcc) tail -12 $log ;;
         rocprof) python3 tools/rocprof_timed_mean.py $OUT/rocprof 2>&1 | tail -8 ;;
         *) grep '^{' $log > $OUT/$name.json; summ $OUT/$name.json ;;
     esac
