@@ -27,8 +27,15 @@ static_assert((kStatSlots & (kStatSlots - 1)) == 0, "stats slots: a power of two
 // staging stores and the "far" fill past the last partner), then a term list of 2*lcap + 64.
 __host__ __device__ constexpr int subsweep_stride(int lcap) { return (lcap + 32 + 63) / 64 * 64; }
 __host__ __device__ constexpr int lds_floats_per_wave(int lcap) { return 3 * subsweep_stride(lcap) + 2 * lcap + 64; }
-constexpr int kMainCap = 224;       // main launch: lds_floats_per_wave(224) * 4 B = 5120 B (32 waves/CU)
-static_assert(lds_floats_per_wave(kMainCap) * 4 <= 5120, "main-launch LDS per wave");
+#ifndef PMC_MAIN_CAP
+#define PMC_MAIN_CAP 224
+#endif
+#ifndef PMC_MAIN_WAVES
+#define PMC_MAIN_WAVES 8   // main launch: waves per SIMD the LDS slot and the register budget are sized for
+#endif
+constexpr int kMainCap = PMC_MAIN_CAP;   // main launch: lds_floats_per_wave(224) * 4 B = 5120 B (32 waves/CU)
+constexpr int kMainWaves = PMC_MAIN_WAVES;
+static_assert(lds_floats_per_wave(kMainCap) * 4 * 4 * kMainWaves <= 160 * 1024, "main-launch LDS per wave");
 constexpr int kStatCounters = 4;    // de_fixed, accepted, trials, evaluated
 // Stats layout.  PMC_STATS_LANES = 1: slot-major, the 4 counters of a slot adjacent (32 B), so a
 // cell's four counter adds are ONE wave instruction on lanes 0-3 (one 32-B memory-side atomic

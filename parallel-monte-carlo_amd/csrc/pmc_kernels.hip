@@ -1070,7 +1070,7 @@ __device__ __forceinline__ void subsweep_pair(const DevGeom& g, float* __restric
 // exceeds it is queued in ovf for the fallback).
 // amdgpu_waves_per_eu(8): 8 waves per SIMD (what the 5 KiB LDS slots allow) also bounds the SGPRs
 template <int NSLOT, int NMC, bool OFF32>
-__global__ __launch_bounds__(kWave * kSubWaves) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_subsweep(DevGeom g, float* __restrict__ disk,
+__global__ __launch_bounds__(kWave * kSubWaves) __attribute__((amdgpu_waves_per_eu(PMC_MAIN_WAVES, PMC_MAIN_WAVES))) void k_subsweep(DevGeom g, float* __restrict__ disk,
                                                                   const int16_t* __restrict__ ncnt,
                                                                   int ox, int oy, int oz, uint32_t sweep,
                                                                   unsigned long long* __restrict__ stats,
