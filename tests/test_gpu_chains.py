@@ -32,6 +32,9 @@ def _window(oracle, count):
     (4, (16, 12, 20), 11_000, [(0, 4), (4, 10), (10, 14), (14, 20)]),   # ragged even borders
     (4, (16, 16, 12), 9_000, [(0, 6), (6, 12)]),                         # too thin for 4: two chains
     (2, (16, 16, 16), 10_000, [(0, 8), (8, 16)]),
+    (2, (12, 8, 10), 2_500, [(0, 4), (4, 10)]),          # ragged halves
+    (2, (8, 8, 8), 1_500, [(0, 4), (4, 8)]),              # the thinnest box that still splits
+    (2, (16, 16, 6), 4_000, [(0, 6)]),                    # too thin: one launch per phase
     (1, (16, 16, 16), 10_000, [(0, 16)]),
 ])
 def test_sweep_chains_equal_oracle(oracle, tmp_path, chains, cps, atoms, want):
