@@ -574,6 +574,7 @@ def main() -> int:
         else:
             drv.ctx.init_lattice_global(atoms)         # this rank's planes of the one 128^3 box
         drv.ctx.slab_exchange()
+        drv.verify_transport()                         # IPC at N > 1: halos checked, "auto" may fall back to RCCL
         sim = drv.ctx
 
         def one_sweep(s):

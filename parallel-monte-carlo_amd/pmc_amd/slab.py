@@ -482,6 +482,8 @@ class SlabDriver:
                               nmax=nmax, n_moves=n_moves, seed=seed, flags=flags,
                               stream=stream.cuda_stream if stream is not None else None)
         self.cps_y = cps_y or cps
+        self._rank, self._world, self._group = rank, world, group
+        self._requested = transport
         if local_group is not None:
             if local_group.world != world:
                 raise ValueError("local_group.world != world")
@@ -510,32 +512,74 @@ class SlabDriver:
                 else:
                     transport = "rccl"      # auto: every rank falls back together
             self.transport = transport
-            uid = None
-            if transport == "rccl":
-                import torch
-                lib_path = _rccl_lib_path()
-                if lib_path and not os.environ.get("PMC_RCCL_LIB"):
-                    os.environ["PMC_RCCL_LIB"] = lib_path
-                buf = torch.zeros(128, dtype=torch.uint8)
-                if rank == 0:
-                    buf = torch.tensor(list(comm_unique_id()), dtype=torch.uint8)
-                if world > 1:
-                    import torch.distributed as dist
-                    on = buf.cuda() if dist.get_backend(group) == "nccl" else buf
-                    dist.broadcast(on, src=0, group=group)
-                    buf = on.cpu()
-                uid = bytes(buf.numpy().tobytes())
             if transport != "ipc":
-                self.ctx.slab_init(rank, world, uid)  # RCCL communicator: collective over the ranks
+                self._init_messages(transport)
         if atoms_total and lattice_cps_z:
             self.ctx.init_lattice_planes(atoms_total, lattice_cps_z)
-            self.ctx.slab_exchange()
         elif atoms_total:
             self.ctx.init_lattice_global(atoms_total)
-            self.ctx.slab_exchange()
         elif atoms_per_rank:
             self.ctx.init_lattice(atoms_per_rank)
+        if atoms_total or atoms_per_rank:
             self.ctx.slab_exchange()
+            self.verify_transport()
+
+    def verify_transport(self) -> None:
+        """Right after a full exchange (pmc_slab_exchange) of a non-trivial state: with the IPC transport
+        at world > 1, check every halo against the plane its neighbour sent (IPC between distinct GPUs
+        has only run on the driver's node); on a mismatch or a timed-out wait, "auto" falls back to RCCL
+        on every rank (and exchanges again), "ipc" raises.  PMC_IPC_VERIFY=0 skips it.  Collective."""
+        if self.transport != "ipc" or self._world == 1 or os.environ.get("PMC_IPC_VERIFY", "1") == "0":
+            return
+        if self._halos_verified():
+            return
+        if self._requested != "auto":
+            raise RuntimeError("IPC halo transport: the first exchange delivered wrong halos")
+        self.transport = "rccl"
+        self._init_messages("rccl")   # (pmc_slab_init re-attaches: the IPC slab is dropped)
+        self.ctx.slab_exchange()
+
+    def _init_messages(self, transport: str) -> None:
+        """pmc_slab_init with RCCL (a communicator from a unique id broadcast over the group) or, for
+        one rank, local copies.  Collective over the ranks."""
+        from .engine import comm_unique_id
+        rank, world, group = self._rank, self._world, self._group
+        uid = None
+        if transport == "rccl":
+            import torch
+            lib_path = _rccl_lib_path()
+            if lib_path and not os.environ.get("PMC_RCCL_LIB"):
+                os.environ["PMC_RCCL_LIB"] = lib_path
+            buf = torch.zeros(128, dtype=torch.uint8)
+            if rank == 0:
+                buf = torch.tensor(list(comm_unique_id()), dtype=torch.uint8)
+            if world > 1:
+                import torch.distributed as dist
+                on = buf.cuda() if dist.get_backend(group) == "nccl" else buf
+                dist.broadcast(on, src=0, group=group)
+                buf = on.cpu()
+            uid = bytes(buf.numpy().tobytes())
+        self.ctx.slab_init(rank, world, uid)  # RCCL communicator: collective over the ranks
+
+    def _halos_verified(self) -> bool:
+        """After an exchange: every rank's halo planes equal the planes its neighbours sent (digests
+        gathered over the group) and no transfer wait timed out (error bit 512).  Collective."""
+        import hashlib
+        self.ctx.synchronize()
+        timed_out = bool(self.ctx.error_flags() & 512)
+        d, n = self.ctx.copy_out()
+        plane, row, h, nz = self.g.cps * self.cps_y, 3 * self.g.nmax, self.halo, self.g.nz
+
+        def digest(z):   # local plane z (halo planes: -1, nz)
+            a = (z + h) * plane
+            return hashlib.sha1(d[a * row:(a + plane) * row].tobytes() + n[a:a + plane].tobytes()).digest()[:16]
+        mine = digest(0) + digest(nz - 1) + digest(-1) + digest(nz)
+        allv = _all_gather_bytes(mine, self._world, self._group)
+        w = self._world
+        part = [[b[16 * i:16 * (i + 1)] for i in range(4)] for b in allv]   # bottom, top, halo below, halo above
+        ok = not timed_out and all(part[r][3] == part[(r + 1) % w][0] and part[r][2] == part[(r - 1) % w][1]
+                                   for r in range(w))
+        return _all_ok(ok, w, self._group)
 
     def sweep(self, s: int) -> None:
         self.ctx.slab_sweep(s)

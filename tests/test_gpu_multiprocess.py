@@ -22,6 +22,7 @@ pytestmark = pytest.mark.gpu
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 WORKER = os.path.join(REPO, "tests", "mp_slab_worker.py")
+VERIFY_WORKER = os.path.join(REPO, "tests", "mp_verify_worker.py")
 
 
 def _window(oracle, count):
@@ -129,3 +130,16 @@ def test_bench_rank_processes_same_device(pmc, world):
     par = d["parity"]
     assert par["state_bitwise_equal"] and par["counters_equal"], par
     assert par["energy_rel_err"] == 0.0 and par["acceptance_rel_err"] == 0.0, par
+
+
+def test_ipc_halo_verification(pmc, tmp_path):
+    """SlabDriver.verify_transport's check (every halo equals the plane its neighbour sent, digests
+    gathered over gloo): true after the IPC exchange of two rank processes, false on every rank once
+    one float of one halo differs, true again after the next exchange.  (bench.py --transport auto
+    falls back to RCCL on every rank when it fails: IPC between distinct GPUs runs first on the
+    driver's node.)"""
+    _run_processes(2, [VERIFY_WORKER, str(tmp_path)])
+    for r in range(2):
+        with open(tmp_path / f"rank{r}.json") as f:
+            j = json.load(f)
+        assert j == {"transport": "ipc", "after_init": True, "after_corruption": False, "after_exchange": True}, (r, j)
