@@ -537,6 +537,8 @@ class SlabDriver:
             raise RuntimeError("IPC halo transport: the first exchange delivered wrong halos")
         self.transport = "rccl"
         self._init_messages("rccl")   # (pmc_slab_init re-attaches: the IPC slab is dropped)
+        self.ctx.synchronize()
+        self.ctx.error_flags(reset=True)   # the failed transport's timeout bit, not the state's
         self.ctx.slab_exchange()
 
     def _init_messages(self, transport: str) -> None:
