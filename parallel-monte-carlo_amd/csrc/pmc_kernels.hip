@@ -1405,6 +1405,9 @@ __global__ __launch_bounds__(kWave) void k_sweep_small(DevGeom g, float* __restr
 #define PMC_SHIFT_THREADS 256   // k_shift workgroup size
 #endif
 constexpr int kShiftThreads = PMC_SHIFT_THREADS;
+#ifndef PMC_SHIFT_LINES
+#define PMC_SHIFT_LINES 1   // k_shift_run stores whole 64-B lines of each output record from LDS (0: per slot)
+#endif
 #ifndef PMC_SHIFT_RUN_LEN
 #define PMC_SHIFT_RUN_LEN 4
 #endif
@@ -1628,6 +1631,10 @@ __global__ __launch_bounds__(kShiftThreads) void k_shift_run(DevGeom g, const fl
     uint32_t c[R];
     int cid[R], ncur[R];
     float own[R][3];
+#if PMC_SHIFT_LINES
+    __shared__ __attribute__((aligned(16))) float sh_rec[(kShiftThreads / NSLOT) * 3 * NSLOT];
+    const bool lines = PMC_AOS && (3 * nm) % 4 == 0 && 3 * nm <= 4 * NSLOT;   // whole 16-B units per record
+#endif
 #pragma unroll
     for (int j = 0; j < R; ++j) {
         c[j] = cell_of(j, cid[j]);
@@ -1685,6 +1692,40 @@ __global__ __launch_bounds__(kShiftThreads) void k_shift_run(DevGeom g, const fl
             else
                 return dout + (uint64_t)c[j] * (uint64_t)(3 * nm) + (uint64_t)e;
         };
+#if PMC_SHIFT_LINES
+        if (lines) {
+            // the output record assembled in LDS, then stored as whole 64-B lines (16-B units up to the
+            // line that holds the last occupied slot): no partially written line reaches the memory side
+            float* rec = sh_rec + (threadIdx.x / NSLOT) * (3 * NSLOT);
+            // slots past the count go out as zeros (stale scratch there measured slower for the next
+            // phases, profiles/r05x1_shift_lines_ab.txt)
+            rec[3 * p] = 0.0f;
+            rec[3 * p + 1] = 0.0f;
+            rec[3 * p + 2] = 0.0f;
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            if (keep) {
+                const int dst = __popcll(km & below);
+#pragma unroll
+                for (int dim = 0; dim < 3; ++dim) rec[3 * dst + dim] = (dim == f) ? D + offset : own[j][dim];
+            }
+            if (take) {
+                const int dst = nk + __popcll(tm & below);
+                if (dst < nm) {
+#pragma unroll
+                    for (int dim = 0; dim < 3; ++dim) rec[3 * dst + dim] = (dim == f) ? ((Dn + offset) + s) : nbv[dim];
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            const int nw = nnew > nm ? nm : nnew;
+            const int units = (12 * nw + 63) / 64 * 4;
+            if (j < L && p < units) {
+                const uint4 v = *reinterpret_cast<const uint4*>(rec + 4 * p);
+                *reinterpret_cast<uint4*>(out_at(0) + 4 * p) = v;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // the next cell reuses rec
+        } else
+#endif
+        {
         if (keep) {
             const int dst = __popcll(km & below);
             if (dst < nm) {
@@ -1701,6 +1742,7 @@ __global__ __launch_bounds__(kShiftThreads) void k_shift_run(DevGeom g, const fl
                 for (int dim = 0; dim < 3; ++dim)   // own offset (VS shiftCells.h:96)
                     shift_store(q + dim * lay_dim(nm), (dim == f) ? ((Dn + offset) + s) : nbv[dim]);
             }
+        }
         }
         if (j < L && p == 0) {
             if constexpr (OFF32)
