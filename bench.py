@@ -147,7 +147,11 @@ def cpu_baseline(disk, n, cps: int, sweep0: int, serial_planes: int, cps_z: int 
     Returns the JSON object and the oracle state after (ii) for the parity leg."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import pmc_oracle  # test infrastructure: timed CPU baseline only
-    pmc_oracle.build()
+    try:
+        build_flags = pmc_oracle.use_native()     # compiled for this host (SURVEY.md 8d: -march=native)
+    except Exception as e:
+        pmc_oracle.build()
+        build_flags = f"-O3 -march=x86-64-v3 -ffp-contract=off -fopenmp (native build failed: {e!r})"
     host = host_cpu()
     cps_z = cps_z or cps
     box = f"{cps}^3" if cps_z == cps else f"{cps}x{cps}x{cps_z}"
@@ -199,7 +203,7 @@ def cpu_baseline(disk, n, cps: int, sweep0: int, serial_planes: int, cps_z: int 
            "socket_estimate_note": ("measured" if threads >= cores_socket else
                                     f"linear extrapolation of the measured {threads}-thread rate to the "
                                     f"{cores_socket} cores of one socket (upper bound)"),
-           "omp_threads_reported": used, "host": host}
+           "omp_threads_reported": used, "host": host, "build": build_flags}
     return out, st
 
 
@@ -230,15 +234,56 @@ def parity_leg(sim, one_sweep, disk0, n0, sweep0: int, sweeps: int, e0: float, o
             "counters_equal": g == c, "state_bitwise_equal": same}
 
 
-def parity_leg_slab(ctx, one_sweep, finish, disk_s, n_s, sweep0: int, e0: float, gather, ost, rank: int) -> dict | None:
+def z_shift_window(seed: int, first: int, sweeps: int, w: float = 2.5, search: int = 4096) -> int:
+    """The first sweep index s0 >= first whose `sweeps` consecutive sweeps shift along z in both
+    directions (kernel.cu:683-684's f, d from the per-sweep plan): a slab parity leg over that window
+    checks every exchange kind on the node -- the run boundaries' planes, a z shift's deferred plane
+    from above and from below.  `first` itself when sweeps < 2 or no window is found."""
+    if sweeps < 2:
+        return first
+    from pmc_amd.plan import sweep_plan
+    sign = []
+    for s in range(first, first + search + sweeps):
+        _, f, d = sweep_plan(seed, s, w)
+        sign.append(0 if f != 2 else (1 if d > 0 else -1))
+    for k in range(search):
+        win = sign[k:k + sweeps]
+        if 1 in win and -1 in win:
+            return first + k
+    return first
+
+
+def z_shifts(seed: int, s0: int, sweeps: int, w: float = 2.5) -> list:
+    from pmc_amd.plan import sweep_plan
+    out = []
+    for s in range(s0, s0 + sweeps):
+        _, f, d = sweep_plan(seed, s, w)
+        out.append("xyz"[f] + ("+" if d > 0 else "-"))
+    return out
+
+
+def achievable_hbm(nbytes: int = 1 << 30, reps: int = 10) -> dict:
+    """the HBM rate this box actually delivers, beside the 8 TB/s spec -- the
+    library's streaming kernels (pmc_hbm_probe: 16-B loads, 16 workgroups of 256 per CU) over 1 GiB
+    buffers, HIP events, best of `reps`: a read-only pass and a copy (read + write counted)."""
+    import pmc_amd
+    read, copy = pmc_amd.hbm_probe(nbytes, reps)
+    return {"read_GBs": read, "copy_GBs": copy, "bytes": nbytes, "reps": reps,
+            "method": "pmc_hbm_probe: streaming read of 1 GiB (16-B loads) and copy of 1 GiB (read + write "
+                      "counted), HIP events, best of reps"}
+
+
+def parity_leg_slab(ctx, one_sweep, finish, disk_s, n_s, sweep0: int, e0: float, gather, ost, rank: int,
+                    sweeps: int = 1) -> dict | None:
     """parity_leg for the slab driver, collective over the ranks: every rank restores its storage
-    (owned planes and halos) at the timed start, reruns the CPU sample's sweep, the whole box's
+    (owned planes and halos) at the timed start, reruns the CPU sample's sweeps, the whole box's
     counters and energy come from pmc_slab_observables (fixed-point sums over the ranks), the owned
     planes are gathered on rank 0 and compared with the oracle's whole-box result there."""
     ctx.copy_in(disk_s, n_s)
     ctx.slab_exchange()
     ctx.stats(reset=True)
-    one_sweep(sweep0)
+    for k in range(sweeps):
+        one_sweep(sweep0 + k)
     finish()
     ctx.synchronize()
     g, e_gpu = ctx.slab_observables(True)
@@ -256,7 +301,8 @@ def parity_leg_slab(ctx, one_sweep, finish, disk_s, n_s, sweep0: int, e0: float,
     acc_c = c["accepted"] / c["trials"] if c["trials"] else 0.0
     rel = lambda a, b: abs(a - b) / abs(b) if b else abs(a - b)  # noqa: E731
     return {"reference": "C oracle (corrected-mode restatement of subsweep.h / shiftCells.h), whole box",
-            "sweeps": 1, "first_sweep": sweep0, "energy_start": e0,
+            "sweeps": sweeps, "first_sweep": sweep0, "shifts": z_shifts(ctx.params.seed, sweep0, sweeps),
+            "energy_start": e0,
             "energy_gpu": e_gpu, "energy_cpu": e_cpu, "energy_rel_err": rel(e_gpu, e_cpu),
             "acceptance_gpu": acc_g, "acceptance_cpu": acc_c, "acceptance_rel_err": rel(acc_g, acc_c),
             "counters_equal": g == c, "state_bitwise_equal": same,
@@ -471,6 +517,8 @@ def main() -> int:
                          "every rank).  Default: auto at N > 1, local for one-rank slabs (config 5: rccl)")
     ap.add_argument("--same-device", action="store_true",
                     help="all ranks on GPU 0 (a multi-process correctness run on one GPU; needs the ipc transport)")
+    ap.add_argument("--no-hbm-probe", action="store_true",
+                    help="skip the achievable-HBM copy/read measurement (roofline.achievable_peak)")
     ap.add_argument("--rank-timeout", type=float, default=1500.0,
                     help="--gpus N without a launcher: stop the ranks after this many seconds")
     args = ap.parse_args()
@@ -699,6 +747,21 @@ def main() -> int:
         pt = torch.tensor([particles], dtype=torch.int64)
         dist.all_reduce(pt)
         particles = int(pt.item())
+    # node roofline (north_star: "fraction of the HBM roofline at 1, 2, 4 and 8 GPUs"): the staged
+    # model's bytes of one step summed over the ranks -- every owned cell's visit plus
+    # shiftCells' 36 B per particle + 6 B per cell -- over the step time, against N x 8 TB/s
+    if config == "2":
+        step_bytes_local = sub_launch_bytes
+        step_shift_local = 0.0
+    else:
+        step_bytes_local = staged_bytes(n_owned, stencil)
+        step_shift_local = float(36 * int(n_owned.sum()) + 6 * n_owned.size)
+    sb = torch.tensor([step_bytes_local, step_shift_local], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(sb)
+    step_bytes, step_shift_bytes = (float(v) for v in sb.tolist())
+    # the rate this box actually delivers, measured on rank 0's GPU
+    hbm_meas = achievable_hbm() if (rank == 0 and not args.no_hbm_probe) else None
 
     if rank == 0:
         n_launch = tm["n_subsweep"]
@@ -753,6 +816,21 @@ def main() -> int:
                             if valu else None),
                 "boundary_launch_ms": tm["boundary_ms"] / tm["n_boundary"] if tm["n_boundary"] else None,
                 "algorithmic_bytes_per_launch": sub_launch_bytes}
+        ms_step = elapsed / args.steps
+        node_ach = (step_bytes + step_shift_bytes) / ms_step / 1e9
+        roof["node"] = {
+            "achieved": node_ach, "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
+            "frac": node_ach / (HBM_PEAK_GBS * world),
+            "bytes_per_step": step_bytes + step_shift_bytes, "subsweep_bytes_per_step": step_bytes,
+            "shift_bytes_per_step": step_shift_bytes, "gpus": world,
+            "model": ("sum over ranks of the staged model's bytes of one step (every owned non-empty cell: "
+                      "12 B x stencil particles + 54 B of counts + 12 B x own particles written; shiftCells "
+                      "36 B per particle + 6 B per cell) / ms_per_step, against N x 8 TB/s")}
+        if hbm_meas:
+            roof["achievable_peak"] = hbm_meas
+            # the subsweep reads ~25x what it writes: its achievable roof is the read rate
+            roof["frac_of_achievable"] = (achieved / hbm_meas["read_GBs"]) if achieved else None
+            roof["node"]["frac_of_achievable"] = node_ach / (hbm_meas["read_GBs"] * world)
     # CPU baseline and parity leg (after the timed region).  Slabs: the start state of the timed
     # region is gathered on rank 0 (the whole box), the oracle runs there while the other ranks wait,
     # then every rank reruns the sample's sweep (collective) and rank 0 compares.
@@ -776,9 +854,13 @@ def main() -> int:
         else:
             gather = make_gather(world, rank, plane, nz_local, 3 * 16, drv.halo)
             whole = gather(disk_h, n_h)
+            # the sample: --cpu-sweeps sweeps from the timed start state, at the first sweep indices that
+            # shift along z both ways (every exchange kind, the deferred z planes included, on the node)
+            cs = max(1, args.cpu_sweeps)
+            s0 = z_shift_window(sim.params.seed, first, cs)
             if rank == 0:
                 try:
-                    cpu, ost = cpu_baseline(whole[0], whole[1], cps, first, sp, cps_z=box_z)
+                    cpu, ost = cpu_baseline(whole[0], whole[1], cps, s0, sp, cps_z=box_z, sweeps=cs)
                     cpu["sample"] += f" (whole {cps}x{cps}x{box_z} box gathered from {world} rank(s))"
                 except Exception as e:
                     cpu = {"error": repr(e)}
@@ -788,7 +870,8 @@ def main() -> int:
             if world > 1:
                 dist.broadcast(ok, src=0)
             if int(ok.item()):
-                parity = parity_leg_slab(sim, one_sweep, finish, disk_h, n_h, first, e_start, gather, ost, rank)
+                parity = parity_leg_slab(sim, one_sweep, finish, disk_h, n_h, s0, e_start, gather, ost, rank,
+                                         sweeps=cs)
 
     if rank == 0:
         sweeps_per_s = args.steps / elapsed / (8.0 if config == "2" else 1.0)

@@ -241,7 +241,9 @@ int pmc_slab_exchange(pmc_ctx* ctx);
 /* One full sweep (8 colour phases with halo exchange + shiftCells + halo refresh).  Asynchronous;
  * collective (every rank calls it with the same sweep index). */
 int pmc_slab_sweep(pmc_ctx* ctx, uint32_t sweep);
-/* Order the context stream after the outstanding exchanges (before reading state or halos). */
+/* Order the context stream after the outstanding exchanges (before reading state or halos).  With
+ * the IPC transport it also synchronises and returns PMC_ERR_HIP when a wait timed out (error bit 9):
+ * a timed-out exchange copies nothing and the run's state is void. */
 int pmc_slab_finish(pmc_ctx* ctx);
 /* The interior chains of pmc_slab_sweep: *n_chains chains, chain j over local planes
  * [borders[j], borders[j+1]) (borders[0] = 1, borders[*n_chains] = nz_local - 1). */
@@ -315,7 +317,8 @@ int pmc_energy(pmc_ctx* ctx, double* e_out);
 /* Read and optionally reset the accumulated subsweep statistics (synchronises). */
 int pmc_stats_read(pmc_ctx* ctx, pmc_stats* out, int reset);
 /* Device error flags (bit 0: shift overflow, bit 1: assign overflow, bit 2: assign range, bits 3-4:
- * pmc_run_small; bit 9: an IPC-transport wait timed out);
+ * pmc_run_small; bit 9: an IPC-transport wait timed out; bit 10: the IPC sender's L2 write-back did
+ * not cover all 8 XCDs);
  * synchronises; `reset` clears them. */
 int pmc_error_flags(pmc_ctx* ctx, uint32_t* flags, int reset);
 
@@ -336,6 +339,10 @@ int pmc_plane_span(const pmc_ctx* ctx, int z_local, size_t* disk_off, size_t* di
  * h_out_d[2*count] = acceptance threshold + fixed-point energy.  Used by the parity tests to pin
  * host == device bit equality of every transcendental the kernels use. */
 int pmc_selftest_detmath(const uint32_t* h_words, int count, float* h_out_f, double* h_out_d);
+/* The HBM rate this GPU delivers (beside the 8 TB/s spec): best of `reps`
+ * passes of a streaming read of `bytes` (16-B loads, nothing written) and of a copy of `bytes`
+ * (read + write counted), GB/s; two buffers of `bytes` (>= 16 MiB) on the current device. */
+int pmc_hbm_probe(uint64_t bytes, int reps, double* read_gbs, double* copy_gbs);
 
 /* ---- trajectory dump / restart ---------------------------------- */
 /* The reference's visualisation path is host code: disk_to_r + create_dump
@@ -377,6 +384,20 @@ int pmc_dump_frame(pmc_ctx* ctx, const char* path, int append, int64_t timestep)
 int pmc_save_snapshot(pmc_ctx* ctx, const char* path, uint32_t next_sweep);
 /* Restores state + statistics; PMC_ERR_ARG if the snapshot's parameters differ from the ctx's. */
 int pmc_load_snapshot(pmc_ctx* ctx, const char* path, uint32_t* next_sweep);
+
+/* ---- environment switches read by the library (none is needed in production) ----------
+ * Operational:      PMC_IPC_TIMEOUT_S (IPC wait limit, default 60), PMC_LOCAL_GROUP_TIMEOUT_MS,
+ *                   PMC_RCCL_LIB (librccl path; SlabDriver sets torch's).
+ * Schedule A/B:     PMC_SWEEP_CHAINS, PMC_SLAB_CHAINS, PMC_SLAB_PRIORITY, PMC_SLAB_B_FIRST,
+ *                   PMC_SLAB_SPLIT_SHIFT, PMC_SLAB_DEFER_Z, PMC_SLAB_DIRECT_HALO, PMC_BOUNDARY_FULL,
+ *                   PMC_IPC_FUSED, PMC_SMALL, PMC_SMALL_LAUNCH, PMC_DIRECT_CELLS, PMC_FALLBACK_BLOCKS,
+ *                   PMC_SHIFT_RUN, PMC_SHIFT_OFF32, PMC_ENERGY_LEGACY, PMC_ENERGY_ROWS_CAP: every
+ *                   setting gives the same bits (the GPU tests run the non-default ones); DESIGN.md
+ *                   records which were measured and why the default won.
+ * Test hooks:       PMC_SUBSWEEP_CAP (forces the overflow-queue fallback), PMC_FORCE_ADDR64 (64-bit
+ *                   addressing below 4 GiB).
+ * Timing only:      PMC_XFER_DELAY_US (a one-GPU rehearsal's stand-in for xGMI time per exchange;
+ *                   changes no result). */
 
 #ifdef __cplusplus
 }

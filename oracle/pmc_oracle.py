@@ -49,6 +49,21 @@ def build(force: bool = False) -> str:
     return LIB_PATH
 
 
+def use_native() -> str:
+    """Switch this process to the -march=native build of the same source (bench.py's timed CPU
+    baseline), compiled on the host that runs it (make native: a few seconds).  Must precede the
+    first lib() call.  Returns the flags used; raises if gcc fails (the caller keeps the portable
+    build then)."""
+    global LIB_PATH
+    if _lib is not None:
+        raise RuntimeError("the oracle library is already loaded")
+    path = os.path.join(HERE, "build", "liborc_native.so")
+    # rebuilt every time: a native build from another host must not be reused
+    subprocess.run(["make", "-C", HERE, "-B", "native"], check=True, capture_output=True)
+    LIB_PATH = path
+    return "-O3 -march=native -ffp-contract=off -fopenmp"
+
+
 _lib = None
 
 _f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")

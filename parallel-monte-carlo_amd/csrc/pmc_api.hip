@@ -958,6 +958,51 @@ int pmc_selftest_detmath(const uint32_t* h_words, int count, float* h_out_f, dou
     return e == hipSuccess ? PMC_OK : hip_fail(e, "selftest");
 }
 
+int pmc_hbm_probe(uint64_t bytes, int reps, double* read_gbs, double* copy_gbs) {
+    if (!read_gbs || !copy_gbs || reps < 1 || bytes < ((uint64_t)1 << 24)) return fail(PMC_ERR_ARG, "bad argument");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(PMC_ERR_NODEV, "no HIP device");
+    bytes &= ~(uint64_t)4095;
+    int dev = 0, cus = 0;
+    PMC_HIP(hipGetDevice(&dev));
+    PMC_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const int blocks = (cus > 0 ? cus : 256) * 16;   // 16 workgroups of 256 per CU: full occupancy
+    void *a = nullptr, *b = nullptr, *sink = nullptr;
+    hipStream_t st = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    hipError_t e = hipMalloc(&a, bytes);
+    if (e == hipSuccess) e = hipMalloc(&b, bytes);
+    if (e == hipSuccess) e = hipMalloc(&sink, sizeof(uint32_t) * (size_t)blocks);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreate(&e0);
+    if (e == hipSuccess) e = hipEventCreate(&e1);
+    if (e == hipSuccess) e = hipMemsetAsync(a, 0x5a, bytes, st);
+    double best[2] = {0.0, 0.0};
+    for (int kind = 0; kind < 2 && e == hipSuccess; ++kind) {
+        e = launch_hbm_probe(kind, a, b, bytes, (uint32_t*)sink, blocks, st);   // warm-up
+        for (int r = 0; r < reps && e == hipSuccess; ++r) {
+            e = hipEventRecord(e0, st);
+            if (e == hipSuccess) e = launch_hbm_probe(kind, a, b, bytes, (uint32_t*)sink, blocks, st);
+            if (e == hipSuccess) e = hipEventRecord(e1, st);
+            if (e == hipSuccess) e = hipEventSynchronize(e1);
+            float ms = 0.0f;
+            if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+            const double gbs = (kind == 0 ? 1.0 : 2.0) * (double)bytes / ((double)ms * 1e-3) / 1e9;
+            if (e == hipSuccess && ms > 0.0f && gbs > best[kind]) best[kind] = gbs;
+        }
+    }
+    if (st) (void)hipStreamSynchronize(st);
+    for (void* p : {a, b, sink})
+        if (p) (void)hipFree(p);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (st) (void)hipStreamDestroy(st);
+    if (e != hipSuccess) return hip_fail(e, "hbm probe");
+    *read_gbs = best[0];
+    *copy_gbs = best[1];
+    return PMC_OK;
+}
+
 }  // extern "C"
 
 // ---- trajectory dump / restart (kernel.cu:497-536; pmc_io.cpp holds the host formats) ----------
@@ -2351,7 +2396,16 @@ int pmc_slab_layout(pmc_ctx* c, int* n_chains, int borders[4]) {
 int pmc_slab_finish(pmc_ctx* c) {
     if (!c || !c->slab) return fail(PMC_ERR_ARG, "no slab driver (pmc_slab_init)");
     if (int rc = slab_flush_z(c)) return rc;
-    return slab_join(c);
+    if (int rc = slab_join(c)) return rc;
+    if (c->slab->ipc) {
+        // a timed-out IPC wait (error bit 9) means some halo was not copied: the run is void
+        PMC_HIP(hipStreamSynchronize(c->stream));
+        uint32_t fl = 0;
+        PMC_HIP(hipMemcpy(&fl, c->flags, 4, hipMemcpyDeviceToHost));
+        if (fl & 512u) return fail(PMC_ERR_HIP, "IPC transport: a peer did not arrive (wait timed out, error flag 512)");
+        if (fl & 1024u) return fail(PMC_ERR_HIP, "IPC transport: an XCD's L2 was not written back before ready (error flag 1024)");
+    }
+    return PMC_OK;
 }
 
 int pmc_slab_observables(pmc_ctx* c, int with_energy, pmc_stats* out, double* e_out) {

@@ -1717,7 +1717,11 @@ __global__ __launch_bounds__(kShiftThreads) void k_shift_run(DevGeom g, const fl
             }
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             const int nw = nnew > nm ? nm : nnew;
-            const int units = (12 * nw + 63) / 64 * 4;
+            // whole lines counted from the record's start, capped at the record's own 3*nm/4 units: a
+            // record that is not a whole number of lines (nm = 4, 8, 12, 20, ...) never spills into
+            // the next cell's record or past the buffer
+            int units = (12 * nw + 63) / 64 * 4;
+            if (units > 3 * nm / 4) units = 3 * nm / 4;
             if (j < L && p < units) {
                 const uint4 v = *reinterpret_cast<const uint4*>(rec + 4 * p);
                 *reinterpret_cast<uint4*>(out_at(0) + 4 * p) = v;
@@ -2573,6 +2577,48 @@ hipError_t launch_relayout(const float* src, float* dst, int64_t cells, int nmax
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------------
+// HBM probe (pmc_hbm_probe): the rate this GPU actually delivers, beside the
+// 8 TB/s spec.  Streaming 16-B loads (and stores), four independent per lane in flight, grid-stride
+// over a buffer far larger than the caches (MALL 256 MB): read -- each block folds its words into one
+// xor written at the end (nothing else written); copy -- read + write the same amount.
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_hbm_read(const uint4* __restrict__ src, uint64_t n, uint32_t* __restrict__ sink) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t acc = 0;
+    for (; i + 3 * stride < n; i += 4 * stride) {
+        const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+        acc ^= a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ d.x ^ d.y ^ d.z ^ d.w;
+    }
+    for (; i < n; i += stride) {
+        const uint4 a = src[i];
+        acc ^= a.x ^ a.y ^ a.z ^ a.w;
+    }
+    if (acc == 0x9E3779B9u) sink[blockIdx.x] = acc;   // (keeps the loads; practically never stores)
+}
+
+__global__ void __launch_bounds__(256) k_hbm_copy(const uint4* __restrict__ src, uint4* __restrict__ dst, uint64_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n; i += 4 * stride) {
+        const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+        dst[i] = a;
+        dst[i + stride] = b;
+        dst[i + 2 * stride] = c;
+        dst[i + 3 * stride] = d;
+    }
+    for (; i < n; i += stride) dst[i] = src[i];
+}
+
+hipError_t launch_hbm_probe(int kind, const void* src, void* dst, uint64_t bytes, uint32_t* sink, int blocks,
+                            hipStream_t st) {
+    const uint64_t n = bytes / 16;
+    if (kind == 0) hipLaunchKernelGGL(k_hbm_read, dim3(blocks), dim3(256), 0, st, (const uint4*)src, n, sink);
+    else hipLaunchKernelGGL(k_hbm_copy, dim3(blocks), dim3(256), 0, st, (const uint4*)src, (uint4*)dst, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_spin(double us, hipStream_t st) {
     const uint64_t ticks = us > 0.0 ? (uint64_t)(us * 100.0) : 0;   // s_memrealtime: 100 MHz
     if (ticks > 100000000ull) return hipErrorInvalidValue;          // at most 1 s
@@ -2621,11 +2667,42 @@ __device__ __forceinline__ bool flags_wait(const XferFlags& w, uint64_t timeout,
     return true;
 }
 
+// Publish ready = seq for a peer on ANOTHER GPU to pull this rank's buffers.  The planes were written
+// by earlier kernels, whose end-of-kernel release is only guaranteed to reach agent scope: dirty lines
+// may sit in any of the 8 XCDs' L2s, invisible to a peer reading this GPU's HBM over xGMI.  So every
+// block's thread 0 first writes back its XCD's L2 (system-scope release: buffer_wbl2 sc0 sc1) and
+// checks in (count, and the XCC_ID bit in a mask); block 0 waits for all blocks, then stores the flag.
+// The grid has >= 8 blocks: the dispatcher deals them round-robin over the XCDs, and the mask proves
+// that every XCD wrote back (error bit 10, value 1024, if one did not).  wb[0]: count, wb[2]: mask.
+__device__ __forceinline__ void publish_ready(uint64_t* ready, uint64_t seq, unsigned* wb, uint64_t timeout,
+                                              uint32_t* err) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    __hip_atomic_fetch_or(wb + 2, 1u << (xcc & 7u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_fetch_add(wb, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (blockIdx.x != 0) return;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(wb, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < gridDim.x) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
+            atomicOr(err, 512u);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    if (__hip_atomic_load(wb + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0xFFu) atomicOr(err, 1024u);
+    __hip_atomic_store(wb, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(wb + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    flag_store(ready, seq);
+}
+
+// mine: publish ready (grid >= 8, publish_ready) then wait for w; no mine: wait only (one block)
 __global__ void __launch_bounds__(kWave) k_xfer_flag(uint64_t* mine, uint64_t seq, XferFlags w, uint64_t timeout,
-                                                      uint32_t* err) {
+                                                      uint32_t* err, unsigned* wb) {
     if (threadIdx.x != 0) return;
-    if (mine) flag_store(mine, seq);
-    (void)flags_wait(w, timeout, err);
+    if (mine) publish_ready(mine, seq, wb, timeout, err);
+    if (blockIdx.x == 0) (void)flags_wait(w, timeout, err);
 }
 
 template <class U>
@@ -2653,24 +2730,35 @@ __device__ __forceinline__ void xfer_units(const XferSeg& s, int shift) {
 // L2s by the cache probes of the PTE C-bit, AMDGPU memory model, gfx942 family) before the block's
 // threads read past the workgroup barrier.  Grid <= 64 blocks: waiting blocks hold wave slots, and
 // several rank processes may share one GPU.
+constexpr unsigned kXferMinBlocks = 8;   // publish_ready: one block per XCD at least
+
 template <bool WAIT>
 __global__ void __launch_bounds__(256) k_xfer(XferCopy cp, uint64_t* pulled, uint64_t seq, unsigned* done,
                                                XferFlags w, uint64_t* ready, uint64_t timeout, uint32_t* err) {
-    if constexpr (WAIT) {
-        if (threadIdx.x == 0) {
-            if (blockIdx.x == 0) flag_store(ready, seq);
-            (void)flags_wait(w, timeout, err);
+    // A wait that timed out (this launch's, or k_xfer_flag's before a split copy) leaves error bit 9
+    // set: the block then copies nothing -- the peer's buffer may be mid-write -- and "pulled" is not
+    // published, so no peer overwrites buffers this rank has not read; from then on every exchange of
+    // this rank and its peers times out too, and pmc_slab_finish / the observables report the error.
+    __shared__ int go;
+    if (threadIdx.x == 0) {
+        bool ok = true;
+        if constexpr (WAIT) {
+            publish_ready(ready, seq, done + 2, timeout, err);
+            ok = flags_wait(w, timeout, err);
         }
-        __syncthreads();
+        go = ok && (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 512u) == 0;
     }
-    for (int k = 0; k < cp.n; ++k) {
-        const XferSeg& s = cp.seg[k];
-        switch (s.shift) {
-            case 4: xfer_units<uint4>(s, 4); break;
-            case 3: xfer_units<uint2>(s, 3); break;
-            case 2: xfer_units<uint32_t>(s, 2); break;
-            case 1: xfer_units<uint16_t>(s, 1); break;
-            default: xfer_units<uint8_t>(s, 0); break;
+    __syncthreads();
+    if (go) {
+        for (int k = 0; k < cp.n; ++k) {
+            const XferSeg& s = cp.seg[k];
+            switch (s.shift) {
+                case 4: xfer_units<uint4>(s, 4); break;
+                case 3: xfer_units<uint2>(s, 3); break;
+                case 2: xfer_units<uint32_t>(s, 2); break;
+                case 1: xfer_units<uint16_t>(s, 1); break;
+                default: xfer_units<uint8_t>(s, 0); break;
+            }
         }
     }
     __syncthreads();                      // every load of this block has returned (its stores used them)
@@ -2678,7 +2766,8 @@ __global__ void __launch_bounds__(256) k_xfer(XferCopy cp, uint64_t* pulled, uin
         const unsigned prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
         if (prev == gridDim.x - 1) {
             __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            flag_store(pulled, seq);
+            if ((__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 512u) == 0)
+                flag_store(pulled, seq);
         }
     }
 }
@@ -2688,7 +2777,8 @@ __global__ void __launch_bounds__(256) k_xfer(XferCopy cp, uint64_t* pulled, uin
 hipError_t launch_xfer_flag(uint64_t* mine, uint64_t seq, const XferFlags& w, uint64_t timeout_ticks, uint32_t* err,
                             hipStream_t st) {
     if (w.n < 0 || w.n > kXferMax) return hipErrorInvalidValue;   // (seq: the value stored to mine)
-    hipLaunchKernelGGL(k_xfer_flag, dim3(1), dim3(kWave), 0, st, mine, seq, w, timeout_ticks, err);
+    if (mine) return hipErrorInvalidValue;   // wait only (a ready flag is published by launch_xfer's grid)
+    hipLaunchKernelGGL(k_xfer_flag, dim3(1), dim3(kWave), 0, st, mine, seq, w, timeout_ticks, err, (unsigned*)nullptr);
     return hipGetLastError();
 }
 
@@ -2712,11 +2802,12 @@ hipError_t launch_xfer(const XferCopy& cp, const XferFlags& w, uint64_t* ready, 
     }();
     const uint64_t want = (units + 1023) / 1024;
     if (fused) {
-        const unsigned blocks = (unsigned)(want < 1 ? 1 : want > 64 ? 64 : want);
+        const unsigned blocks = (unsigned)(want < kXferMinBlocks ? kXferMinBlocks : want > 64 ? 64 : want);
         hipLaunchKernelGGL(k_xfer<true>, dim3(blocks), dim3(256), 0, st, cp, pulled, seq, done, w, ready, timeout_ticks,
                            err);
     } else {
-        hipLaunchKernelGGL(k_xfer_flag, dim3(1), dim3(kWave), 0, st, ready, seq, w, timeout_ticks, err);
+        hipLaunchKernelGGL(k_xfer_flag, dim3(kXferMinBlocks), dim3(kWave), 0, st, ready, seq, w, timeout_ticks, err,
+                           done + 2);
         const unsigned blocks = (unsigned)(want < 1 ? 1 : want > 256 ? 256 : want);
         hipLaunchKernelGGL(k_xfer<false>, dim3(blocks), dim3(256), 0, st, cp, pulled, seq, done, w, ready,
                            timeout_ticks, err);

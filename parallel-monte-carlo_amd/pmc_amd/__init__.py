@@ -4,6 +4,6 @@ Host mirror of qingye3/parallel-monte-carlo's call surface over the C ABI in inc
 the compute runs in hand-written HIP kernels for gfx950 (csrc/).  See DESIGN.md.
 """
 from ._lib import PmcError, build, lib  # noqa: F401
-from .engine import PmcContext, colour_offset, device_count, selftest_detmath  # noqa: F401
+from .engine import PmcContext, colour_offset, device_count, hbm_probe, selftest_detmath  # noqa: F401
 
-__all__ = ["PmcContext", "PmcError", "build", "lib", "colour_offset", "device_count", "selftest_detmath"]
+__all__ = ["PmcContext", "PmcError", "build", "lib", "colour_offset", "device_count", "hbm_probe", "selftest_detmath"]

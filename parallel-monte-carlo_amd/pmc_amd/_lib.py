@@ -152,6 +152,7 @@ def lib():
         _sig(L, "pmc_plane_span", i32, _vp, i32, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t),
              C.POINTER(C.c_size_t), C.POINTER(C.c_size_t))
         _sig(L, "pmc_selftest_detmath", i32, _vp, i32, _vp, _vp)
+        _sig(L, "pmc_hbm_probe", i32, C.c_uint64, i32, _vp, _vp)
         # trajectory dump / restart (host formats need no GPU)
         cp, f3 = C.c_char_p, C.POINTER(C.c_float * 3)
         _sig(L, "pmc_disk_to_r", i32, _vp, _vp, i64, i32, _vp, i64, C.POINTER(i64))

@@ -386,3 +386,12 @@ def selftest_detmath(words: np.ndarray):
     check("pmc_selftest_detmath", lib().pmc_selftest_detmath(words.ctypes.data, cnt, out_f.ctypes.data,
                                                              out_d.ctypes.data))
     return out_f.reshape(cnt, 4), out_d.reshape(cnt, 2)
+
+
+def hbm_probe(nbytes: int = 1 << 30, reps: int = 10) -> tuple:
+    """(read GB/s, copy GB/s): the library's streaming read and copy kernels over `nbytes`, best of
+    `reps` (pmc_hbm_probe; SURVEY.md Appendix D's achievable peak beside the 8 TB/s spec)."""
+    r = C.c_double()
+    cp = C.c_double()
+    check("pmc_hbm_probe", lib().pmc_hbm_probe(nbytes, reps, C.byref(r), C.byref(cp)))
+    return r.value, cp.value

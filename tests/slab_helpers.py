@@ -6,7 +6,8 @@ import numpy as np
 import torch
 
 import pmc_oracle
-from pmc_amd.slab import SlabGeometry, SlabSimulation, TorchP2P
+from pmc_amd.slab import SlabGeometry
+from slab_legacy import SlabSimulation, TorchP2P
 
 
 class OracleEngine:

@@ -77,7 +77,7 @@ def test_start_driver_save_restart(pmc, tmp_path):
 def test_gpu_slab_snapshot_restart(pmc, oracle, tmp_path):
     """The RCCL slab driver's restart (one rank: halos are local copies) on the HIP engine."""
     import torch
-    from pmc_amd.slab import SlabSimulation
+    from slab_legacy import SlabSimulation
     path = str(tmp_path / "slab.pmcsnap")
     a = SlabSimulation.create(cps=16, nz_local=16, rank=0, world=1, atoms_per_rank=10_000)
     a.run(0, 2)

@@ -130,6 +130,16 @@ def test_bench_rank_processes_same_device(pmc, world):
     par = d["parity"]
     assert par["state_bitwise_equal"] and par["counters_equal"], par
     assert par["energy_rel_err"] == 0.0 and par["acceptance_rel_err"] == 0.0, par
+    # the parity leg covers --cpu-sweeps (3) sweeps chosen to shift along z both ways: every exchange
+    # kind, the deferred z planes from above and below included
+    assert par["sweeps"] == 3 and "z+" in par["shifts"] and "z-" in par["shifts"], par
+    assert d["cpu_baseline"]["sample"].startswith("3 full sweeps"), d["cpu_baseline"]["sample"]
+    # the whole-node HBM roofline: every rank's staged-model bytes of a step over ms_per_step, N x 8 TB/s
+    node = d["roofline"]["node"]
+    assert node["gpus"] == world and node["peak"] == 8000.0 * world, node
+    assert node["bytes_per_step"] > 0 and 0 < node["frac"] < 1, node
+    hb = d["roofline"]["achievable_peak"]
+    assert 500 < hb["copy_GBs"] < 8000 and 500 < hb["read_GBs"] < 8000, hb
 
 
 def test_ipc_halo_verification(pmc, tmp_path):

@@ -144,6 +144,53 @@ def test_shift_sizes_parity(pmc, oracle, cps, atoms, f, d):
     assert oracle.valid_slots_equal(got_d, got_n, st.disk, st.n, 16)
 
 
+@pytest.mark.parametrize("nmax", [8, 12, 20, 24])
+@pytest.mark.parametrize("f,d", [(0, 0.9), (1, -0.6), (2, 1.1), (2, -1.2)])
+def test_shift_nmax_not_whole_lines_parity(pmc, oracle, nmax, f, d):
+    """shiftCells on the packed layout where a cell's record (12*nmax bytes) is not a whole number of
+    64-B lines: the whole-line store path must stop at the record's end (at nmax 8 a
+    cell of 6+ particles rounds up to 128 B of a 96-B record).  The output buffer carries a guard
+    tail that must stay untouched."""
+    import torch
+    cps, atoms = 10, (1800 if nmax == 8 else 2600)
+    ctx = _ctx(pmc, cps, nmax=nmax)
+    ctx.init_lattice(atoms)
+    ctx.start(0, 1)
+    disk, n = ctx.copy_out()
+    st = _ostate(oracle, cps, nmax=nmax)
+    st.disk[:] = disk
+    st.n[:] = n
+    dev = torch.device("cuda")
+    guard = 64
+    din = torch.from_numpy(disk).to(dev)
+    nin = torch.from_numpy(n).to(dev)
+    dbuf = torch.full((disk.size + guard,), 7.0, dtype=torch.float32, device=dev)
+    dout = dbuf[:disk.size]
+    nout = torch.zeros_like(nin)
+    ctx.shiftCells(din, nin, dout, nout, f, d)
+    ctx.synchronize()
+    assert st.shift_cells(f, d) == 0
+    got_d, got_n = dout.cpu().numpy(), nout.cpu().numpy()
+    assert np.array_equal(got_n, st.n)
+    assert oracle.valid_slots_equal(got_d, got_n, st.disk, st.n, nmax)
+    assert np.all(dbuf[disk.size:].cpu().numpy() == 7.0), "shiftCells wrote past the output buffer"
+
+
+@pytest.mark.parametrize("nmax", [8, 12])
+def test_full_sweeps_nmax_parity(pmc, oracle, nmax):
+    """Whole sweeps (8 phases + shiftCells in the context's packed state) at nmax 8 and 12."""
+    cps, atoms = 12, (3000 if nmax == 8 else 4300)
+    ctx = _ctx(pmc, cps, nmax=nmax)
+    ctx.init_lattice(atoms)
+    r = ctx.start(0, 3)
+    st = _ostate(oracle, cps, nmax=nmax)
+    st.init_lattice(atoms)
+    st.run(0, 3)
+    _assert_same(oracle, ctx, st, nmax)
+    o = st.stats.as_dict()
+    assert r["accepted"] == o["accepted"] and r["trials"] == o["trials"], (r, o)
+
+
 def test_full_sweeps_parity_16(pmc, oracle):
     ctx = _ctx(pmc, 16)
     ctx.init_lattice(10_000)
@@ -473,7 +520,7 @@ def test_gpu_slab_single_rank_equals_whole_box(pmc, nz, atoms, two_streams):
     with one rank reproduces the whole-box run bit for bit -- with the boundary planes on their
     own stream beside the interior (the multi-GPU schedule) and with the one-stream schedule."""
     import torch
-    from pmc_amd.slab import SlabSimulation
+    from slab_legacy import SlabSimulation
     sim = SlabSimulation.create(cps=16, nz_local=nz, rank=0, world=1, atoms_per_rank=atoms)
     if not two_streams:
         sim.bstream = None

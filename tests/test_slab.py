@@ -1,5 +1,5 @@
 """The LEGACY per-colour slab schedule on CPU: 2-4 gloo rank processes drive the oracle through
-SlabSimulation (pmc_amd/slab.py), the Python twin of round 1's schedule -- a halo exchange after every
+SlabSimulation (tests/slab_legacy.py), the Python twin of round 1's schedule -- a halo exchange after every
 colour phase over torch.distributed.  It is not the product's schedule: the product multi-GPU path is
 the C slab driver (pmc_slab_sweep: runs of equal z parity, one exchange per run, deferred z planes),
 whose rank PROCESSES are tested on the GPU against the oracle through the IPC transport
@@ -57,7 +57,7 @@ def test_slab_ranks_equal_whole_box(oracle, world, nz, first, sweeps):
 
 def test_slab_single_rank_periodic(oracle):
     """world == 1 slab (halo planes filled by local copies) equals the whole box."""
-    from pmc_amd.slab import TorchP2P
+    from slab_legacy import TorchP2P
     sim = slab_helpers.make_oracle_slab(8, 8, 0, 1, 16, 1500, TorchP2P(0, 1))
     d0, n0 = sim.owned()
     st = slab_helpers.whole_box_from_slabs(8, 8, 1, 16, [d0.numpy().copy()], [n0.numpy().copy()])

@@ -17,7 +17,8 @@
 #                    default local), injected exchange delay us
 #   mp2bench         bench.py --gpus 2 --same-device --config 4 (rank processes, IPC); mp4bench, mp8bench: 4, 8
 #   rocprof          rocprofv3 --kernel-trace --stats of the default bench command
-#   trace8           rocprofv3 kernel trace of the 8-rank IPC rehearsal + tools/timeline_stats.py
+#   trace8[d<us>]    rocprofv3 kernel trace of the 8-rank IPC rehearsal (injected exchange delay us) +
+#                    tools/timeline_stats.py
 #   py:<file>        python tools/<file> (analysis scripts, e.g. stamps.py with PMC_LIB_PATH=...@py:stamps.py)
 #   tcc | sq | shcnt | slabtcc  counter passes: k_subsweep traffic (tools/tcc_traffic.sh), its SQ
 #                    instruction mix (tools/sq_counters.sh), shiftCells traffic + wave states
@@ -81,9 +82,11 @@ for spec in "$@"; do
         rocprof) export TMPDIR=/tmp; timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
                 -d $OUT/rocprof -o bench -- python3 bench.py --steps 20 --warmup 5 > $log 2>&1 ;;
         py:*) timeout -k 10 300 python tools/${step#py:} > $log 2>&1 ;;
-        trace8) export TMPDIR=/tmp; timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace8 -o run \
-                -- python3 bench.py --config 4 --emulate-ranks 8 --transport ipc --no-cpu-baseline --steps 40 --warmup 10 \
-                > $log 2>&1 && python3 tools/timeline_stats.py $OUT/trace8/run_kernel_trace.csv 20 > $OUT/trace8_timeline.txt 2>&1 ;;
+        trace8*) dl=${step#trace8}; dl=${dl#d}; dl=${dl:-0}; export TMPDIR=/tmp
+            timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $OUT/$name -o run \
+                -- python3 bench.py --config 4 --emulate-ranks 8 --transport ipc --xfer-delay-us $dl --no-cpu-baseline \
+                --steps 40 --warmup 10 > $log 2>&1 \
+                && python3 tools/timeline_stats.py $OUT/$name/run_kernel_trace.csv 20 > $OUT/${name}_timeline.txt 2>&1 ;;
         tcc) timeout -k 10 600 bash tools/tcc_traffic.sh ${TAG}_$name > $log 2>&1 ;;
         sq) timeout -k 10 500 bash tools/sq_counters.sh $TAG > $log 2>&1 ;;
         shcnt) timeout -k 10 700 bash tools/shift_counters.sh $TAG > $log 2>&1 ;;
@@ -96,7 +99,7 @@ for spec in "$@"; do
     case $step in
         tests*|mp|smoke) tail -1 $log ;;
         py:*) tail -25 $log ;;
-        trace8) cat $OUT/trace8_timeline.txt | head -40 ;;
+        trace8*) head -40 $OUT/${name}_timeline.txt ;;
         tcc|sq|shcnt|slabtcc) tail -12 $log ;;
         rocprof) python3 tools/rocprof_timed_mean.py $OUT/rocprof 2>&1 | tail -8 ;;
         *) grep '^{' $log > $OUT/$name.json; summ $OUT/$name.json ;;

@@ -55,7 +55,8 @@ def main() -> int:
     import torch.distributed as dist
     import pmc_amd
     from pmc_amd.plan import sweep_plan
-    from pmc_amd.slab import SlabSimulation, TorchP2P
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from slab_legacy import SlabSimulation, TorchP2P
 
     cps, R = args.cps, args.ranks
     nz = cps // R
