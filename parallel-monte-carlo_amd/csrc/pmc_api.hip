@@ -2179,6 +2179,9 @@ int slab_sweep_h2(pmc_ctx* c, uint32_t sweep) {
 
 extern "C" {
 
+#ifndef PMC_SLAB_INTERLEAVE
+#define PMC_SLAB_INTERLEAVE 1   // pmc_slab_sweep issues a run phase by phase across the chains (0: chain by chain)
+#endif
 int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
     if (!c || !c->slab) return fail(PMC_ERR_ARG, "no slab driver (pmc_slab_init)");
     if (c->P.halo == 2) return slab_sweep_h2(c, sweep);
@@ -2296,6 +2299,34 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
             s->pending_zdir = 0;
             return PMC_OK;
         };
+#if PMC_SLAB_INTERLEAVE
+        // Issue order phase by phase across the chains (B's phase, then each interior chain's), B's
+        // exchange right after its last phase.  The host issues a rank sweep in about the time the
+        // GPU runs it (8 ranks: 16-plane slabs), so chain by chain (B's 4 phases and exchange, then
+        // all of L, then all of U) left the last chain's first launch ~10 API calls behind the
+        // others' every run (kernel trace: U started as L's run was ending, profiles/r06a_*).
+        if (!first) {
+            const int zb = q == 0 ? 0 : nz - 1;
+            if ((rc = border_waits(kB, zb, zb + 1, q, T, p))) return rc;
+            for (int j = 0; j < nc; ++j)
+                if ((rc = border_waits(j, zs[j], zs[j + 1], q, ist[j], p))) return rc;
+        }
+        for (int kk = k; kk < k1; ++kk) {
+            const int zb = q == 0 ? 0 : nz - 1;
+            if ((rc = phases(T, c->ovf_b, zb, zb + 1, kk, kk + 1, true))) return rc;
+            if (kk == k1 - 1) {
+                PMC_HIP(hipEventRecord(s->ev_run[kB][q], T));
+                if ((rc = slab_exchange_run(c, q, merge_z, direct_halo))) return rc;
+                merge_z = false;
+                s->pending_zdir = 0;
+            }
+            for (int j = 0; j < nc; ++j)
+                if (zs[j + 1] > zs[j] && (rc = phases(ist[j], iovf[j], zs[j], zs[j + 1], kk, kk + 1, false))) return rc;
+        }
+        for (int j = 0; j < nc; ++j) PMC_HIP(hipEventRecord(s->ev_run[j][q], ist[j]));
+        (void)b_first;
+        (void)boundary;
+#else
         if (b_first && (rc = boundary())) return rc;
         for (int j = 0; j < nc; ++j) {
             if (!first && (rc = border_waits(j, zs[j], zs[j + 1], q, ist[j], p))) return rc;
@@ -2305,6 +2336,7 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
             PMC_HIP(hipEventRecord(s->ev_run[j][q], ist[j]));
         }
         if (!b_first && (rc = boundary())) return rc;
+#endif
         k = k1;
     }
     // after the 8 phases both halo planes are exact copies of the neighbours' planes, so

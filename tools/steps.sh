@@ -7,6 +7,7 @@
 #   tests            the whole -m gpu suite
 #   tests:<pattern>  pytest -m gpu -k <pattern>
 #   mp               tests/test_gpu_multiprocess.py (rank processes over the IPC transport)
+#   file:<path>      one GPU test file
 #   smoke            __graft_entry__.smoke()
 #   bench            default bench line (config 3, the driver's --steps 20 --warmup 5)
 #   bench2           config 2 (pmc_phase_seq blocks); bench2pc: one pmc_phase call per step
@@ -60,6 +61,7 @@ for spec in "$@"; do
         tests) timeout -k 10 900 $PYT tests -m gpu > $log 2>&1 ;;
         tests:*) timeout -k 10 600 $PYT tests -m gpu -k "${step#tests:}" > $log 2>&1 ;;
         mp) timeout -k 10 600 $PYT tests/test_gpu_multiprocess.py -m gpu > $log 2>&1 ;;
+        file:*) timeout -k 10 700 $PYT ${step#file:} -m gpu > $log 2>&1 ;;
         smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $log 2>&1 ;;
         bench) timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $log 2>&1 ;;
         bench2) timeout -k 10 300 python bench.py --config 2 --steps 160 --warmup 8 > $log 2>&1 ;;
@@ -97,7 +99,7 @@ for spec in "$@"; do
     for e in "${envs[@]}"; do unset "${e%%=*}"; done
     if [ $rc -ne 0 ]; then echo "step $spec failed rc $rc"; tail -40 $log; exit $rc; fi
     case $step in
-        tests*|mp|smoke) tail -1 $log ;;
+        tests*|mp|smoke|file:*) tail -1 $log ;;
         py:*) tail -25 $log ;;
         trace8*) head -40 $OUT/${name}_timeline.txt ;;
         tcc|sq|shcnt|slabtcc) tail -12 $log ;;
