@@ -966,23 +966,25 @@ int pmc_hbm_probe(uint64_t bytes, int reps, double* read_gbs, double* copy_gbs) 
     int dev = 0, cus = 0;
     PMC_HIP(hipGetDevice(&dev));
     PMC_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    const int blocks = (cus > 0 ? cus : 256) * 16;   // 16 workgroups of 256 per CU: full occupancy
+    const int ncu = cus > 0 ? cus : 256;
     void *a = nullptr, *b = nullptr, *sink = nullptr;
     hipStream_t st = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     hipError_t e = hipMalloc(&a, bytes);
     if (e == hipSuccess) e = hipMalloc(&b, bytes);
-    if (e == hipSuccess) e = hipMalloc(&sink, sizeof(uint32_t) * (size_t)blocks);
+    if (e == hipSuccess) e = hipMalloc(&sink, sizeof(uint32_t) * (size_t)ncu * 16);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreate(&e0);
     if (e == hipSuccess) e = hipEventCreate(&e1);
     if (e == hipSuccess) e = hipMemsetAsync(a, 0x5a, bytes, st);
+    // best over the shapes: 4 / 8 / 16 workgroups of 256 per CU, 4 or 8 loads in flight per lane
     double best[2] = {0.0, 0.0};
-    for (int kind = 0; kind < 2 && e == hipSuccess; ++kind) {
-        e = launch_hbm_probe(kind, a, b, bytes, (uint32_t*)sink, blocks, st);   // warm-up
+    for (int cfg = 0; cfg < 12 && e == hipSuccess; ++cfg) {
+        const int kind = cfg / 6, unroll = (cfg / 3) % 2 ? 8 : 4, blocks = ncu * (4 << (cfg % 3));
+        e = launch_hbm_probe(kind, unroll, a, b, bytes, (uint32_t*)sink, blocks, st);   // warm-up
         for (int r = 0; r < reps && e == hipSuccess; ++r) {
             e = hipEventRecord(e0, st);
-            if (e == hipSuccess) e = launch_hbm_probe(kind, a, b, bytes, (uint32_t*)sink, blocks, st);
+            if (e == hipSuccess) e = launch_hbm_probe(kind, unroll, a, b, bytes, (uint32_t*)sink, blocks, st);
             if (e == hipSuccess) e = hipEventRecord(e1, st);
             if (e == hipSuccess) e = hipEventSynchronize(e1);
             float ms = 0.0f;

@@ -153,9 +153,9 @@ hipError_t launch_colour_rows(const DevGeom& g, const float* src, float* dst, in
 hipError_t launch_relayout(const float* src, float* dst, int64_t cells, int nmax, int to_state, hipStream_t st);
 // rehearsal only: a one-wave kernel that occupies `st` for `us` microseconds (injected exchange delay)
 hipError_t launch_spin(double us, hipStream_t st);
-// pmc_hbm_probe: kind 0 streams `bytes` of src (reads only), 1 copies src -> dst
-hipError_t launch_hbm_probe(int kind, const void* src, void* dst, uint64_t bytes, uint32_t* sink, int blocks,
-                            hipStream_t st);
+// pmc_hbm_probe: kind 0 streams `bytes` of src (reads only), 1 copies src -> dst; unroll 4 or 8
+hipError_t launch_hbm_probe(int kind, int unroll, const void* src, void* dst, uint64_t bytes, uint32_t* sink,
+                            int blocks, hipStream_t st);
 // IPC halo transport (pmc_kernels.hip, pmc_slab_init_ipc): sequence flags and the pull copy
 constexpr int kXferMax = 16;       // flags waited on / segments copied per launch (peers <= 16)
 struct XferFlags {

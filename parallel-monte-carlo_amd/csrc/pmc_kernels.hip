@@ -2581,15 +2581,20 @@ hipError_t launch_relayout(const float* src, float* dst, int64_t cells, int nmax
 // HBM probe (pmc_hbm_probe): the rate this GPU actually delivers, beside the
 // 8 TB/s spec.  Streaming 16-B loads (and stores), four independent per lane in flight, grid-stride
 // over a buffer far larger than the caches (MALL 256 MB): read -- each block folds its words into one
-// xor written at the end (nothing else written); copy -- read + write the same amount.
+// xor written at the end (nothing else written); copy -- read + write the same amount.  U loads in
+// flight per lane before their use.
 // ------------------------------------------------------------------------------------------
+template <int U>
 __global__ void __launch_bounds__(256) k_hbm_read(const uint4* __restrict__ src, uint64_t n, uint32_t* __restrict__ sink) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t acc = 0;
-    for (; i + 3 * stride < n; i += 4 * stride) {
-        const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
-        acc ^= a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ d.x ^ d.y ^ d.z ^ d.w;
+    for (; i + (U - 1) * stride < n; i += U * stride) {
+        uint4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = src[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
     }
     for (; i < n; i += stride) {
         const uint4 a = src[i];
@@ -2598,24 +2603,32 @@ __global__ void __launch_bounds__(256) k_hbm_read(const uint4* __restrict__ src,
     if (acc == 0x9E3779B9u) sink[blockIdx.x] = acc;   // (keeps the loads; practically never stores)
 }
 
+template <int U>
 __global__ void __launch_bounds__(256) k_hbm_copy(const uint4* __restrict__ src, uint4* __restrict__ dst, uint64_t n) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (; i + 3 * stride < n; i += 4 * stride) {
-        const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
-        dst[i] = a;
-        dst[i + stride] = b;
-        dst[i + 2 * stride] = c;
-        dst[i + 3 * stride] = d;
+    for (; i + (U - 1) * stride < n; i += U * stride) {
+        uint4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = src[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < U; ++u) dst[i + u * stride] = v[u];
     }
     for (; i < n; i += stride) dst[i] = src[i];
 }
 
-hipError_t launch_hbm_probe(int kind, const void* src, void* dst, uint64_t bytes, uint32_t* sink, int blocks,
-                            hipStream_t st) {
+// kind 0 read, 1 copy; unroll 4 or 8 loads in flight per lane
+hipError_t launch_hbm_probe(int kind, int unroll, const void* src, void* dst, uint64_t bytes, uint32_t* sink,
+                            int blocks, hipStream_t st) {
     const uint64_t n = bytes / 16;
-    if (kind == 0) hipLaunchKernelGGL(k_hbm_read, dim3(blocks), dim3(256), 0, st, (const uint4*)src, n, sink);
-    else hipLaunchKernelGGL(k_hbm_copy, dim3(blocks), dim3(256), 0, st, (const uint4*)src, (uint4*)dst, n);
+    const uint4* a = (const uint4*)src;
+    if (kind == 0) {
+        if (unroll == 8) hipLaunchKernelGGL(k_hbm_read<8>, dim3(blocks), dim3(256), 0, st, a, n, sink);
+        else hipLaunchKernelGGL(k_hbm_read<4>, dim3(blocks), dim3(256), 0, st, a, n, sink);
+    } else {
+        if (unroll == 8) hipLaunchKernelGGL(k_hbm_copy<8>, dim3(blocks), dim3(256), 0, st, a, (uint4*)dst, n);
+        else hipLaunchKernelGGL(k_hbm_copy<4>, dim3(blocks), dim3(256), 0, st, a, (uint4*)dst, n);
+    }
     return hipGetLastError();
 }
 
