@@ -972,15 +972,18 @@ int pmc_hbm_probe(uint64_t bytes, int reps, double* read_gbs, double* copy_gbs) 
     hipEvent_t e0 = nullptr, e1 = nullptr;
     hipError_t e = hipMalloc(&a, bytes);
     if (e == hipSuccess) e = hipMalloc(&b, bytes);
-    if (e == hipSuccess) e = hipMalloc(&sink, sizeof(uint32_t) * (size_t)ncu * 16);
+    if (e == hipSuccess) e = hipMalloc(&sink, sizeof(uint32_t) * (size_t)ncu * 32);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreate(&e0);
     if (e == hipSuccess) e = hipEventCreate(&e1);
     if (e == hipSuccess) e = hipMemsetAsync(a, 0x5a, bytes, st);
-    // best over the shapes: 4 / 8 / 16 workgroups of 256 per CU, 4 or 8 loads in flight per lane
+    // best over the shapes that measured fastest (tools/ubench/hbm_stream.hip, profiles/r06h_hbm_stream.txt):
+    // 2 / 8 / 32 workgroups of 256 per CU, 8 nontemporal loads in flight per lane (read), 4 or 8 per
+    // lane in per-workgroup chunks (copy)
     double best[2] = {0.0, 0.0};
     for (int cfg = 0; cfg < 12 && e == hipSuccess; ++cfg) {
-        const int kind = cfg / 6, unroll = (cfg / 3) % 2 ? 8 : 4, blocks = ncu * (4 << (cfg % 3));
+        const int kind = cfg / 6, unroll = kind == 0 || (cfg / 3) % 2 ? 8 : 4;
+        const int blocks = ncu * (cfg % 3 == 0 ? 2 : (cfg % 3 == 1 ? 8 : 32));
         e = launch_hbm_probe(kind, unroll, a, b, bytes, (uint32_t*)sink, blocks, st);   // warm-up
         for (int r = 0; r < reps && e == hipSuccess; ++r) {
             e = hipEventRecord(e0, st);

@@ -2579,7 +2579,7 @@ hipError_t launch_relayout(const float* src, float* dst, int64_t cells, int nmax
 
 // ------------------------------------------------------------------------------------------
 // HBM probe (pmc_hbm_probe): the rate this GPU actually delivers, beside the
-// 8 TB/s spec.  Streaming 16-B loads (and stores), four independent per lane in flight, grid-stride
+// 8 TB/s spec.  Streaming 16-B loads (and stores), several independent per lane in flight
 // over a buffer far larger than the caches (MALL 256 MB): read -- each block folds its words into one
 // xor written at the end (nothing else written); copy -- read + write the same amount.  U loads in
 // flight per lane before their use.
@@ -2590,11 +2590,15 @@ __global__ void __launch_bounds__(256) k_hbm_read(const uint4* __restrict__ src,
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t acc = 0;
     for (; i + (U - 1) * stride < n; i += U * stride) {
-        uint4 v[U];
+        uint32_t v[U][4];
 #pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = src[i + u * stride];
+        for (int u = 0; u < U; ++u) {   // nontemporal: streamed past the caches (fastest, profiles/r06h)
+            const uint32_t* q = reinterpret_cast<const uint32_t*>(src + i + u * stride);
 #pragma unroll
-        for (int u = 0; u < U; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+            for (int w = 0; w < 4; ++w) v[u][w] = __builtin_nontemporal_load(q + w);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc ^= v[u][0] ^ v[u][1] ^ v[u][2] ^ v[u][3];
     }
     for (; i < n; i += stride) {
         const uint4 a = src[i];
@@ -2603,18 +2607,20 @@ __global__ void __launch_bounds__(256) k_hbm_read(const uint4* __restrict__ src,
     if (acc == 0x9E3779B9u) sink[blockIdx.x] = acc;   // (keeps the loads; practically never stores)
 }
 
+// copy: each workgroup streams its own contiguous chunk (faster than grid-stride for copies, r06h)
 template <int U>
 __global__ void __launch_bounds__(256) k_hbm_copy(const uint4* __restrict__ src, uint4* __restrict__ dst, uint64_t n) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (; i + (U - 1) * stride < n; i += U * stride) {
+    const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const uint64_t b0 = (uint64_t)blockIdx.x * per, b1 = b0 + per < n ? b0 + per : n;
+    for (uint64_t i = b0 + threadIdx.x; i < b1; i += U * 256) {
         uint4 v[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = src[i + u * stride];
+        for (int u = 0; u < U; ++u)
+            if (i + u * 256 < b1) v[u] = src[i + u * 256];
 #pragma unroll
-        for (int u = 0; u < U; ++u) dst[i + u * stride] = v[u];
+        for (int u = 0; u < U; ++u)
+            if (i + u * 256 < b1) dst[i + u * 256] = v[u];
     }
-    for (; i < n; i += stride) dst[i] = src[i];
 }
 
 // kind 0 read, 1 copy; unroll 4 or 8 loads in flight per lane
