@@ -216,9 +216,6 @@ __device__ __forceinline__ pmc_u32x4 philox_sched(uint32_t c0, uint32_t c1, uint
 #ifndef PMC_RARE_KEYS
 #define PMC_RARE_KEYS 1
 #endif
-#ifndef PMC_HALF_BLOCK
-#define PMC_HALF_BLOCK 0   // (A/B switch, measured slower) the last partner block in one pass when <= 32
-#endif
 __device__ __forceinline__ pmc_u32x4 philox_rare(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                                  const DevGeom& g) {
 #if PMC_RARE_KEYS
@@ -377,10 +374,8 @@ __device__ __forceinline__ CellGeo cell_geo(const DevGeom& g, int p, int cz0, in
     cg.zg0 = g.z0 + cg.zl;
     // a halo plane visited redundantly (two-plane halos, launch_subsweep_plane) may lie across the
     // periodic z boundary: its global plane, cell id and cell centre are the owner's
-#ifndef PMC_NO_ZG_WRAP   // (A/B builds only: the wrap's cost on the whole-box kernel)
     cg.zg0 += cg.zg0 < 0 ? g.cps_z : 0;
     cg.zg0 -= cg.zg0 >= g.cps_z ? g.cps_z : 0;
-#endif
     const int plane = g.cps_x * g.cps_y;
     cg.c = (uint32_t)(cg.x + g.cps_x * cg.y + plane * (cg.zl + g.halo));
     cg.id = (uint32_t)cg.x + (uint32_t)g.cps_x * ((uint32_t)cg.y + (uint32_t)g.cps_y * (uint32_t)cg.zg0);
@@ -549,11 +544,6 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
 
     // ---- Fisher-Yates shuffle of the own cell (random_shuffle, subsweep.h:50-58; fixes R1) ---
     int perm;
-#ifdef PMC_PROBE_NO_SHUFFLE   // timing probe only (wrong results): the identity instead of Fisher-Yates
-    if (true) {
-        perm = lane;
-    } else
-#endif
     if (n_own <= 16) {
         // the permutation as 16 nibbles of one 64-bit scalar: each swap is a few SALU ops on
         // SGPRs (no VGPR read-modify-write chain through v_readlane), one VALU unpack at the end
@@ -686,17 +676,8 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
     // block code with no per-move loop or bound tests (the full-capacity launches keep the loop).
     auto move_loop = [&](auto nb_c) {
     constexpr int NB = decltype(nb_c)::value;
-#if PMC_HALF_BLOCK
-    // the last 64-partner block holds at most 32 partners (about half the cells at 4.77 per cell:
-    // K ~ 98): its new and old positions share one pass (below)
-    const bool half_last = NB > 0 && K - (NB - 1) * kWave <= 32;
-    const uint32_t hsgn = (uint32_t)(lane & 32) << 26;   // lanes 32-63: the sign bit (old terms)
-#endif
     unsigned long long pend = 0;                       // in-cell moves of the current round
     int sp_l = 0;                                      // lane j: row slot of the round's move j
-#ifdef PMC_PROBE_NO_REPEAT_OLD
-    unsigned long long seen = 0;                       // particles evaluated so far in the visit
-#endif
     for (int m0 = 0; m0 < g.n_moves; m0 += (m0 == 0 ? first_len : 16)) {
         if (m0 > 0) rng_single(m0);
         const int clen = m0 == 0 ? first_len : 16;
@@ -762,26 +743,11 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
                     if (__builtin_amdgcn_inverse_ballot_w64(mo)) buf[mbcnt64_add(mo, cn)] = r2on;
                     C = cn + __popcll(mo);
                 };
-#ifdef PMC_PROBE_NO_REPEAT_OLD
-                // timing probe only (wrong results): a particle's 2nd and later evaluated move of
-                // the visit lists no old-position terms -- the most a cached old energy could save
-                const bool rep = (seen & sbit) != 0ull;
-                seen |= sbit;
-#endif
                 auto block = [&](int base, unsigned long long excl) {
                     // slots >= K hold +inf in x: their r2 is inf, never listed; the moving slot
                     // (block 0) is cleared from the masks by excl
                     const int k = base + lane;
                     const float xj = px_[k], yj = py_[k], zj = pz_[k];
-#ifdef PMC_PROBE_NO_REPEAT_OLD
-                    if (rep) {
-                        const float r2n = pmc_r2(qx - xj, qy - yj, qz - zj);
-                        const unsigned long long mn = __builtin_amdgcn_ballot_w64(r2n <= rc2) & ~excl;
-                        if (__builtin_amdgcn_inverse_ballot_w64(mn)) buf[mbcnt64_add(mn, C)] = r2n;
-                        C += __popcll(mn);
-                        return;
-                    }
-#endif
                     // old-position term computed negated (= -r2o bit for bit, pmc_r2_neg):
                     // listed with its sign bit set at no extra instruction
                     list(pmc_r2(qx - xj, qy - yj, qz - zj), pmc_r2_neg(xi - xj, yi - yj, zi - zj), excl);
@@ -790,27 +756,7 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
 #pragma unroll
                     for (int b = 0; b < NB - 1; ++b) block(b * kWave, b == 0 ? sbit : 0ull);
                     const unsigned long long xl = NB == 1 ? sbit : 0ull;   // the moving slot (block 0)
-#if PMC_HALF_BLOCK
-                    if (half_last) {
-                        // the last block holds at most 32 partners: new (lanes 0-31) and old (lanes
-                        // 32-63) positions of partners base + (lane & 31) in ONE pass -- one r2, one
-                        // compare, one ballot + mbcnt, one store.  Ballot order is lane order, so the
-                        // list is the two-pass one exactly: the block's new terms ascending, then its
-                        // old terms ascending, as -r2 (the sign bit: pmc_r2_neg is -pmc_r2 bit for
-                        // bit, and -r2 >= -rc2 is r2 <= rc2)
-                        const float hx = lane < 32 ? qx : xi, hy = lane < 32 ? qy : yi, hz = lane < 32 ? qz : zi;
-                        const int k = (NB - 1) * kWave + (lane & 31);
-                        const float xj = px_[k], yj = py_[k], zj = pz_[k];
-                        const float r2 = pmc_r2(hx - xj, hy - yj, hz - zj);
-                        const unsigned long long m = __builtin_amdgcn_ballot_w64(r2 <= rc2) & ~(xl | (xl << 32));
-                        if (__builtin_amdgcn_inverse_ballot_w64(m)) buf[mbcnt64_add(m, C)] = as_f(as_i(r2) | hsgn);
-                        C += __popcll(m);
-                    } else {
-                        block((NB - 1) * kWave, xl);
-                    }
-#else
                     block((NB - 1) * kWave, xl);
-#endif
                 } else {
                     block(0, sbit);
                     for (int base = kWave; base < K; base += kWave) block(base, 0ull);
@@ -818,26 +764,6 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
                 // 4b. energies of the listed terms: term t on lane t % 64, ascending t.  The 64
                 // slots after the list get kPad (r2 = 1e30: inv^3 underflows to +0, so the term
                 // is exactly +0 and adding it leaves a lane's sum unchanged) -- no lane mask.
-#if defined(PMC_PAD_VALU) || defined(PMC_PAD_SALU) || defined(PMC_PAD_LDS)
-                {   // analysis builds only: marginal cost of extra independent instructions per move
-                    float pv = (float)lane;
-                    int ps = C;
-#ifdef PMC_PAD_VALU
-#pragma unroll
-                    for (int q = 0; q < PMC_PAD_VALU; ++q) asm volatile("v_add_f32 %0, 1.0, %0" : "+v"(pv));
-#endif
-#ifdef PMC_PAD_SALU
-#pragma unroll
-                    for (int q = 0; q < PMC_PAD_SALU; ++q) asm volatile("s_add_u32 %0, %0, 3" : "+s"(ps) :: "scc");
-#endif
-#ifdef PMC_PAD_LDS
-#pragma unroll
-                    for (int q = 0; q < PMC_PAD_LDS; ++q) asm volatile("ds_read_b32 %0, %1 offset:4" : "=v"(pv) : "v"(0));
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#endif
-                    asm volatile("" :: "v"(pv), "s"(ps));
-                }
-#endif
                 // the serial tail (energy pass, reduction, accept) one priority level above
                 // the rest of the moves (same-box A/B: phase -0.5%, profiles/r03pr_priority_ab.txt)
                 if (kTailPrio) __builtin_amdgcn_s_setprio(kTailPrio);
@@ -901,20 +827,12 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
     }
     // fixed-point conversion only when something was accepted (pmc_to_fixed(0) == 0)
     const int64_t de_fix = n_acc ? pmc_to_fixed(4.0 * de_cell) : 0;
-#ifdef PMC_PROBE_NO_STATS   // timing probe only (the counters stay zero): cost of the stats atomics
-    if (lane == 0 && de_fix == 0x7fffffffffffffffll) {
-#else
     if (PMC_STATS_LANES ? lane < kStatCounters : lane == 0) {
-#endif
         const int slot = t & (kStatSlots - 1);
 #if PMC_STATS_LANES
         // lane k adds counter k: one no-return atomic instruction, 32 contiguous bytes
         const int64_t v = lane == 0 ? de_fix : (lane == 1 ? n_acc : (lane == 2 ? g.n_moves : n_ev));
-#ifdef PMC_PROBE_STATS_STORE   // timing probe only (wrong counters): plain stores instead of the atomics
-        stats[stat_index(lane, slot)] = (unsigned long long)v;
-#else
         atomicAdd(&stats[stat_index(lane, slot)], (unsigned long long)v);
-#endif
 #else
         atomicAdd(&stats[stat_index(0, slot)], (unsigned long long)de_fix);
         atomicAdd(&stats[stat_index(1, slot)], (unsigned long long)n_acc);
@@ -2244,10 +2162,8 @@ __global__ __launch_bounds__(kWave) void k_energy(DevGeom g, const float* __rest
             }
 #endif
         };
-#ifndef PMC_PROBE_NO_PAIRS   // analysis builds only: the per-cell cost without the pair loop
         block(0, std::true_type{});
         for (int jb = kWave; jb < S; jb += kWave) block(jb, std::false_type{});
-#endif
         if (C > 0) drain(C);
     }
     };   // run_cells
@@ -2902,16 +2818,9 @@ static void launch_subsweep_t(const DevGeom& g, float* disk, const int16_t* n, i
         return;
     }
     size_t lds = sizeof(float) * (size_t)lds_floats_per_wave(kMainCap) * kSubWaves;
-#ifdef PMC_PROBE_LDS_MULT   // timing probe only: fewer waves per SIMD through a larger LDS request
-    lds = lds * PMC_PROBE_LDS_MULT / 100;
-#endif
     launch_k(k_subsweep<NSLOT, NMC, OFF32>, dim3((unsigned)blocks), dim3(kWave * kSubWaves), lds, st, tm, g, disk, n,
              ox, oy, oz, sweep, stats, cap, ovf, cz0, ncz);
-#ifdef PMC_PROBE_NO_FALLBACK   // timing probe only (wrong results if a cell overflows)
-    if (false) {
-#else
     if (cap < full) {
-#endif
         const size_t lds_full = sizeof(float) * (size_t)lds_floats_per_wave(full) * kSubWaves;
         hipLaunchKernelGGL((k_subsweep_fallback<NSLOT, NMC, OFF32>), dim3(fallback_blocks()), dim3(kWave * kSubWaves), lds_full, st,
                            g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, (float*)nullptr, 0, 1, stats);
@@ -2940,11 +2849,7 @@ static void launch_direct_t(const DevGeom& g, float* disk, const int16_t* n, int
     const size_t lds = sizeof(float) * (size_t)lds_floats_per_wave(kMainCap) * kSubWaves;
     launch_k(k_subsweep_direct<NSLOT, NMC, OFF32>, dim3((unsigned)blocks), dim3(kWave * kSubWaves), lds, st, tm, g,
              disk, n, ox, oy, oz, sweep, stats, cap, ovf, cz0, ncz, mirror, mode);
-#ifdef PMC_PROBE_NO_FALLBACK   // timing probe only (wrong results if a cell overflows)
-    if (false) {
-#else
     if (cap < full) {
-#endif
         const size_t lds_full = sizeof(float) * (size_t)lds_floats_per_wave(full) * kSubWaves;
         if (mirror)
             hipLaunchKernelGGL((k_subsweep_fallback<NSLOT, NMC, OFF32, true>), dim3(fallback_blocks()),
