@@ -23,6 +23,7 @@ pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 WORKER = os.path.join(REPO, "tests", "mp_slab_worker.py")
 VERIFY_WORKER = os.path.join(REPO, "tests", "mp_verify_worker.py")
+TIMEOUT_WORKER = os.path.join(REPO, "tests", "mp_timeout_worker.py")
 
 
 def _window(oracle, count):
@@ -43,13 +44,13 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run_processes(world, argv, timeout=180):
+def _run_processes(world, argv, timeout=180, ipc_timeout_s="30"):
     """Start `world` rank processes of argv, wait; on failure or timeout kill their process groups."""
     port = str(_free_port())
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=port, PMC_IPC_TIMEOUT_S="30")
+                   MASTER_PORT=port, PMC_IPC_TIMEOUT_S=ipc_timeout_s)
         procs.append(subprocess.Popen([sys.executable] + argv, env=env, start_new_session=True,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     outs = [None] * world
@@ -153,3 +154,18 @@ def test_ipc_halo_verification(pmc, tmp_path):
         with open(tmp_path / f"rank{r}.json") as f:
             j = json.load(f)
         assert j == {"transport": "ipc", "after_init": True, "after_corruption": False, "after_exchange": True}, (r, j)
+
+
+def test_ipc_timeout_fails_not_copies(pmc, tmp_path):
+    """a peer that stops taking part makes every IPC wait give up (PMC_IPC_TIMEOUT_S = 2 s
+    here) without copying and without publishing "pulled"; error bit 9 is set and pmc_slab_finish
+    reports it (PMC_ERR_HIP), within seconds, with no hang.  The silent rank stays alive, so the
+    buffers its peer maps stay valid."""
+    _run_processes(2, [TIMEOUT_WORKER, str(tmp_path)], timeout=150, ipc_timeout_s="2")
+    with open(tmp_path / "rank0.json") as f:
+        j = json.load(f)
+    assert j["transport"] == "ipc"
+    assert "did not arrive" in j["finish"], j
+    assert j["flags"] & 512, j
+    assert j["seconds"] < 90, j
+
