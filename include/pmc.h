@@ -64,6 +64,22 @@ typedef struct pmc_params {
  * parity, then the other 4; spec v9, pmc_detmath.h); PMC_FLAG_FULL_SHUFFLE: one shuffle of all 8
  * colours (the reference's FY_Shuffle, start.cu:34-44). */
 #define PMC_FLAG_FULL_SHUFFLE 1u
+/* Reference quirks (off by default: the build runs the corrected semantics).
+ * Each reproduces one behaviour of the root reference on top of the build's own RNG and ordering:
+ *   PMC_FLAG_QUIRK_R1 -- random_int (subsweep.h:38-40) is always 0, so random_shuffle (:50-58) swaps
+ *                        every slot with slot 0: the own cell is visited in the fixed rotation
+ *                        slot l <- particle (l + 1) mod n instead of a random permutation;
+ *   PMC_FLAG_QUIRK_R2 -- curand_init(1234, id, 0) on every launch (subsweep.h:256-259): a cell draws the
+ *                        same random numbers at every visit (the sweep index is left out of the
+ *                        Philox counters);
+ *   PMC_FLAG_QUIRK_S1 -- int s[3] (shiftCells.h:31,105): the offset added to particles taken from the
+ *                        neighbour cell is (int)(w*dir), -2 / +2 at w = 2.5, instead of w*dir.
+ * With R1 or R2 every colour phase runs the full-capacity one-cell-per-wave kernel (a comparison
+ * mode, not a fast path); two-plane halos and the persistent small-box kernel refuse them. */
+#define PMC_FLAG_QUIRK_R1 2u
+#define PMC_FLAG_QUIRK_R2 4u
+#define PMC_FLAG_QUIRK_S1 8u
+#define PMC_FLAG_QUIRKS (PMC_FLAG_QUIRK_R1 | PMC_FLAG_QUIRK_R2 | PMC_FLAG_QUIRK_S1)
 
 /* Observables accumulated by the subsweep kernels (reference: kernel.cu:228,413-415 --
  * accept_counter and d_Eblocks; the reference never reports acceptance). */

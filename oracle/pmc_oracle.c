@@ -34,7 +34,8 @@ int orc_params_check(pmc_params* p) {
     if ((p->cps_x | p->cps_y | p->cps_z | p->nz_local | p->z0) & 1) return PMC_ERR_ARG;
     if (p->nmax < 1 || p->nmax > 64 || p->n_moves < 0) return PMC_ERR_ARG;
     if (p->halo != 0 && p->halo != 1) return PMC_ERR_ARG;
-    if (p->flags & ~PMC_FLAG_FULL_SHUFFLE) return PMC_ERR_ARG;
+    if (p->flags & ~(PMC_FLAG_FULL_SHUFFLE | PMC_FLAG_QUIRKS)) return PMC_ERR_ARG;
+    if (p->halo == 2 && (p->flags & (PMC_FLAG_QUIRK_R1 | PMC_FLAG_QUIRK_R2))) return PMC_ERR_ARG;
     if (!p->halo && (p->nz_local != p->cps_z || p->z0 != 0)) return PMC_ERR_ARG;
     if (p->z0 < 0 || p->z0 + p->nz_local > p->cps_z) return PMC_ERR_ARG;
     if (!(p->beta >= 0.0f) || isinf(p->beta)) return PMC_ERR_ARG;
@@ -174,10 +175,17 @@ static void subsweep_cell(const pmc_params* p, float* disk, const int16_t* n, in
     const uint32_t id = gid(p, x, y, zl);
     const uint32_t k0 = (uint32_t)p->seed, k1 = (uint32_t)(p->seed >> 32);
     const float Lx = (float)p->cps_x * p->w, Ly = (float)p->cps_y * p->w, Lz = (float)p->cps_z * p->w;
+    /* quirk R2 (curand_init(1234, id, 0) every launch, subsweep.h:256-259): the same numbers at every visit */
+    if (p->flags & PMC_FLAG_QUIRK_R2) sweep = 0;
 
     /* shuffle (random_shuffle, subsweep.h:50-58; proper Fisher-Yates, fixes R1) */
     int perm[64];
     for (int s = 0; s < n_own; ++s) perm[s] = s;
+    if (p->flags & PMC_FLAG_QUIRK_R1) {
+        /* quirk R1: random_int is always 0 (subsweep.h:38-40), so slot i swaps with slot 0 for i = n-1
+         * down to 0 -- the rotation slot l <- particle (l + 1) mod n */
+        for (int s = 0; s < n_own; ++s) perm[s] = s + 1 < n_own ? s + 1 : 0;
+    } else
     for (int i = n_own - 1; i > 0; --i) {
         /* slot i's word: word i & 3 of SHUFFLE call i >> 2 (RNG spec v8, include/pmc_detmath.h) */
         pmc_u32x4 w = pmc_philox4x32_10((uint32_t)(i >> 2), id, sweep, PMC_TAG_SHUFFLE, k0, k1);
@@ -364,7 +372,8 @@ int orc_shift_cells_planes(const pmc_params* p, const float* din, const int16_t*
     const int cps[3] = {p->cps_x, p->cps_y, p->cps_z};
     const float Lf = (float)cps[f] * w;
     const int dir = (d <= 0) ? -1 : 1;               /* VS shiftCells.h:38-44 */
-    const float s = w * (float)dir;                  /* float s (VS copy :28, :83-85) */
+    /* float s (VS copy :28, :83-85); quirk S1: the root copy's int s[3] (shiftCells.h:31,105) */
+    const float s = (p->flags & PMC_FLAG_QUIRK_S1) ? (float)(int)(w * (float)dir) : w * (float)dir;
     const int64_t total = (int64_t)p->cps_x * p->cps_y * (zl_end - zl_begin);
     int over = 0;
 #ifdef _OPENMP

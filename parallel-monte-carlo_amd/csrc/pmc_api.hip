@@ -27,7 +27,7 @@ struct pmc_slab;   // multi-GPU slab driver state (pmc_slab_init)
 struct pmc_ctx {
     pmc_slab* slab = nullptr;
     pmc_params P;
-    DevGeom G;
+    HostGeom G;
     int64_t cells = 0;              // storage cells (incl. halo planes)
     float* disk[2] = {nullptr, nullptr};
     int16_t* n[2] = {nullptr, nullptr};
@@ -115,7 +115,9 @@ int normalise(pmc_params* p) {
     if (p->halo < 0 || p->halo > 2) return fail(PMC_ERR_ARG, "halo must be 0, 1 or 2");
     if (p->halo == 2 && (p->flags & PMC_FLAG_FULL_SHUFFLE))
         return fail(PMC_ERR_ARG, "two-plane halos need the grouped colour order (two runs per sweep)");
-    if (p->flags & ~PMC_FLAG_FULL_SHUFFLE) return fail(PMC_ERR_ARG, "unknown flags");
+    if (p->flags & ~(PMC_FLAG_FULL_SHUFFLE | PMC_FLAG_QUIRKS)) return fail(PMC_ERR_ARG, "unknown flags");
+    if (p->halo == 2 && (p->flags & (PMC_FLAG_QUIRK_R1 | PMC_FLAG_QUIRK_R2)))
+        return fail(PMC_ERR_ARG, "quirks R1/R2 run the full-capacity path, which two-plane halos do not use");
     if (!p->halo && (p->nz_local != p->cps_z || p->z0 != 0))
         return fail(PMC_ERR_ARG, "halo == 0 requires the whole box (nz_local == cps_z, z0 == 0)");
     if (p->z0 < 0 || p->z0 + p->nz_local > p->cps_z) return fail(PMC_ERR_ARG, "slab outside the box");
@@ -128,8 +130,8 @@ int normalise(pmc_params* p) {
     return PMC_OK;
 }
 
-DevGeom make_geom(const pmc_params& p) {
-    DevGeom g;
+HostGeom make_geom(const pmc_params& p) {
+    HostGeom g;
     g.cps_x = p.cps_x; g.cps_y = p.cps_y; g.cps_z = p.cps_z;
     g.nz_local = p.nz_local; g.z0 = p.z0; g.halo = p.halo;
     g.nmax = p.nmax; g.n_moves = p.n_moves;
@@ -149,6 +151,7 @@ DevGeom make_geom(const pmc_params& p) {
     g.div_plane = make_udiv_magic((uint32_t)p.cps_x * (uint32_t)p.cps_y);
     g.k0 = (uint32_t)p.seed;
     g.k1 = (uint32_t)(p.seed >> 32);
+    g.quirks = p.flags & PMC_FLAG_QUIRKS;
     for (int r = 0; r < 10; ++r) {
         g.rk0[r] = g.k0 + (uint32_t)r * PMC_PHILOX_W0;
         g.rk1[r] = g.k1 + (uint32_t)r * PMC_PHILOX_W1;
@@ -567,7 +570,7 @@ int pmc_sweep_plan(uint64_t seed, uint32_t sweep, float w, int order[8], int* f,
 
 int pmc_sweep_plan_ex(uint64_t seed, uint32_t sweep, float w, uint32_t flags, int order[8], int* f, float* d) {
     if (!order || !f || !d) return fail(PMC_ERR_ARG, "null argument");
-    if (flags & ~PMC_FLAG_FULL_SHUFFLE) return fail(PMC_ERR_ARG, "unknown plan flags");
+    if (flags & ~(PMC_FLAG_FULL_SHUFFLE | PMC_FLAG_QUIRKS)) return fail(PMC_ERR_ARG, "unknown plan flags");
     const pmc_sweep_plan_t plan = pmc_plan_for_sweep_ex(seed, sweep, w, flags);
     for (int k = 0; k < 8; ++k) order[k] = plan.order[k];
     *f = plan.f;
@@ -788,7 +791,7 @@ int pmc_error_flags(pmc_ctx* c, uint32_t* flags, int reset) {
 int pmc_run_small(pmc_ctx* c, uint32_t first, int count) {
     if (!c || count < 0) return fail(PMC_ERR_ARG, "bad argument");
     if (small_sweep_participants(c->G) == 0)
-        return fail(PMC_ERR_ARG, "pmc_run_small: the box does not qualify (whole box, nmax 16, <= 2048 cells per colour)");
+        return fail(PMC_ERR_ARG, "pmc_run_small: the box does not qualify (whole box, nmax 16, <= 2048 cells per colour, no quirk flags)");
     if (count == 0) return PMC_OK;
     const unsigned P = (unsigned)small_sweep_participants(c->G);
     // one launch per kSmallSweeps sweeps; after each, the barrier counter (flags word 2; word 0 holds
@@ -2239,7 +2242,9 @@ int pmc_slab_sweep(pmc_ctx* c, uint32_t sweep) {
         const char* v = std::getenv("PMC_SLAB_DIRECT_HALO");
         return v && std::atoi(v) == 1;
     }();
-    const bool direct_halo = direct_halo_env && !s->messages();
+    // (not with quirks R1/R2: their full-capacity path writes no mirror rows)
+    const bool direct_halo = direct_halo_env && !s->messages() &&
+                             !(c->P.flags & (PMC_FLAG_QUIRK_R1 | PMC_FLAG_QUIRK_R2));
     auto phases = [&](hipStream_t st, int* ovf, int z0, int z1, int k0, int k1, bool boundary) -> int {
         float* mir = nullptr;
         if (boundary && direct_halo) mir = disk_plane(c, z0 == 0 ? nz : -1);   // plane 0 -> top halo, nz-1 -> bottom

@@ -90,6 +90,12 @@ struct DevGeom {
     uint32_t k0, k1;
 };
 
+// The host's copy: the kernel arguments plus what only the launchers read.  (The quirk bits select
+// kernel instantiations; keeping them out of DevGeom keeps every kernel's argument block unchanged.)
+struct HostGeom : DevGeom {
+    uint32_t quirks = 0;           // PMC_FLAG_QUIRK_* of pmc_params.flags (0: the corrected semantics)
+};
+
 // Optional timing of one kernel launch: start/stop events carried by the dispatch packet itself
 // (hipExtLaunchKernelGGL: no extra barrier packets between kernels, unlike hipEventRecord).
 struct LaunchTiming {
@@ -99,20 +105,20 @@ struct LaunchTiming {
 // Launchers (pmc_kernels.hip).  All asynchronous on `st`.
 // ovf: int[1 + cells_per_colour] scratch (overflow queue for the full-capacity fallback)
 // only cells in local planes [zl_begin, zl_end) of the colour are visited
-hipError_t launch_subsweep(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
+hipError_t launch_subsweep(const HostGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
                            uint32_t sweep, unsigned long long* stats, int* ovf, int zl_begin, int zl_end,
                            hipStream_t st, const LaunchTiming* tm = nullptr);
 // the slab driver's boundary planes: full LDS capacity (no overflow queue), every written-back row
 // also stored to `mirror` (mirror_mode 0: packed colour rows ta + tb*cps_x/2, 1: plane rows;
 // mirror may be null)
-hipError_t launch_subsweep_boundary(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
+hipError_t launch_subsweep_boundary(const HostGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
                                     uint32_t sweep, unsigned long long* stats, int* ovf, int zl_begin, int zl_end,
                                     float* mirror, int mirror_mode, hipStream_t st,
                                     const LaunchTiming* tm = nullptr);
 // one colour plane zl of the storage, halo planes included (the two-plane-halo slab schedule
 // visits the neighbour's boundary plane redundantly; its cell ids and centres are the owner's):
 // the boundary path, one cell per wave + fallback on `ovf`
-hipError_t launch_subsweep_plane(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
+hipError_t launch_subsweep_plane(const HostGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
                                  uint32_t sweep, unsigned long long* stats, int* ovf, int zl, hipStream_t st,
                                  const LaunchTiming* tm = nullptr);
 // two colour planes zl0 < zl1 of one parity in ONE launch (the two-plane-halo schedule's first run:
@@ -125,15 +131,15 @@ int subsweep_capacity(const DevGeom& g);
 // whole sweeps of a small whole box in one launch on XCD 0 (k_sweep_small); bar: one unsigned of
 // scratch; cur: the current buffer of the (disk, n) pairs; returns hipErrorInvalidValue when the box
 // does not qualify (small_sweep_participants == 0)
-int small_sweep_participants(const DevGeom& g);
-hipError_t launch_sweep_small(const DevGeom& g, float* disk0, int16_t* n0, float* disk1, int16_t* n1, int cur,
+int small_sweep_participants(const HostGeom& g);
+hipError_t launch_sweep_small(const HostGeom& g, float* disk0, int16_t* n0, float* disk1, int16_t* n1, int cur,
                               unsigned long long* stats, uint32_t* flags, unsigned* bar, uint64_t seed,
                               uint32_t first, int count, uint32_t plan_flags, hipStream_t st);
-hipError_t launch_shift(const DevGeom& g, const float* din, const int16_t* nin, float* dout,
+hipError_t launch_shift(const HostGeom& g, const float* din, const int16_t* nin, float* dout,
                         int16_t* nout, int f, float d, uint32_t* flags, hipStream_t st,
                         const LaunchTiming* tm = nullptr);
 // the same over local planes [zl_begin, zl_end), halo planes included (-halo .. nz_local+halo)
-hipError_t launch_shift_planes(const DevGeom& g, const float* din, const int16_t* nin, float* dout,
+hipError_t launch_shift_planes(const HostGeom& g, const float* din, const int16_t* nin, float* dout,
                                int16_t* nout, int f, float d, uint32_t* flags, int zl_begin, int zl_end,
                                hipStream_t st, const LaunchTiming* tm);
 hipError_t launch_init_r(const DevGeom& g, int64_t n_atoms, int64_t n_cube, float* r, hipStream_t st);

@@ -498,7 +498,7 @@ __device__ __forceinline__ int fy_words_single(const DevGeom& g, uint32_t id, ui
 // MIRROR (slab boundary planes): the written-back rows also go to `mirror` -- mirror_mode 0: the
 // packed colour buffer of the halo exchange (row ta + tb*cps_x/2), 1: a plane (row x + cps_x*y;
 // the periodic single-rank halo).  Empty cells write nothing (their count stays 0).
-template <int NSLOT, int NMC, int LCAP, int OFF32, bool MIRROR, int PB = 0>
+template <int NSLOT, int NMC, int LCAP, int OFF32, bool MIRROR, int PB = 0, int QK = 0>
 __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__ disk, uint32_t sweep,
                                            unsigned long long* __restrict__ stats, float* __restrict__ px_,
                                            int lcap_rt, int cap, int t, const CellGeo& cg, int hb, int k_cnt,
@@ -544,7 +544,11 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
 
     // ---- Fisher-Yates shuffle of the own cell (random_shuffle, subsweep.h:50-58; fixes R1) ---
     int perm;
-    if (n_own <= 16) {
+    if (QK & PMC_FLAG_QUIRK_R1) {
+        // quirk R1 (pmc.h): random_int is always 0 (subsweep.h:38-40), so random_shuffle swaps slot i
+        // with slot 0 for i = n-1 .. 0 -- the rotation slot l <- particle (l + 1) mod n
+        perm = lane + 1 < n_own ? lane + 1 : 0;
+    } else if (n_own <= 16) {
         // the permutation as 16 nibbles of one 64-bit scalar: each swap is a few SALU ops on
         // SGPRs (no VGPR read-modify-write chain through v_readlane), one VALU unpack at the end
         uint64_t P = 0xFEDCBA9876543210ull;
@@ -846,7 +850,7 @@ __device__ __forceinline__ bool visit_cell(const DevGeom& g, float* __restrict__
 
 // The single-cell prologue: stencil table on lanes 0-26, the visit's loads, then one RNG pass
 // (moves 0-15 and FY words of slots 0-63) while the loads fly.
-template <int NSLOT, int NMC, int LCAP, int OFF32, bool MIRROR = false, int PB = 0>
+template <int NSLOT, int NMC, int LCAP, int OFF32, bool MIRROR = false, int PB = 0, int QK = 0>
 __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restrict__ disk,
                                               const int16_t* __restrict__ ncnt, int ox, int oy, int oz,
                                               uint32_t sweep, unsigned long long* __restrict__ stats,
@@ -862,6 +866,8 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     float* pz_ = py_ + stride;
     float* buf = pz_ + stride;
     const CellGeo cg = cell_geo(g, t, cz0, ox, oy, oz, 0, 0, czs);
+    // quirk R2 (pmc.h): curand_init(1234, id, 0) on every launch -- the sweep index leaves the counters
+    if (QK & PMC_FLAG_QUIRK_R2) sweep = 0u;
     PMC_STAMP(0);
     const StencilLane sl = stencil_lane(g, cg, lane, cg.edge);
     const int k_cnt = ncnt[sl.kc];
@@ -874,7 +880,7 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     const int jv = fy_words_single(g, cg.id, sweep, buf);
     PMC_STAMP(3);
     if (PB) __builtin_amdgcn_s_setprio(PB);
-    return visit_cell<NSLOT, NMC, LCAP, OFF32, MIRROR, PB>(g, disk, sweep, stats, px_, lcap_rt, cap, t, cg, 0, k_cnt,
+    return visit_cell<NSLOT, NMC, LCAP, OFF32, MIRROR, PB, QK>(g, disk, sweep, stats, px_, lcap_rt, cap, t, cg, 0, k_cnt,
                                                        k_off, sl.sx, sl.sy, sl.sz, ld, jv, 64, 16, mirror,
                                                        mirror_mode);
 }
@@ -1127,7 +1133,7 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_fallback(DevGeom
 // ONE launch -- no fallback launch after it -- and its waves live half as long as the main launch's
 // two-cell waves.  Below a round of the chip's wave slots a phase lasts about one wave lifetime plus
 // the launch, so both halve.  Same per-cell code as every other path: results bit-identical.
-template <int NSLOT, int NMC, bool OFF32, int PB = 0>
+template <int NSLOT, int NMC, bool OFF32, int PB = 0, int QK = 0>
 __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_full(DevGeom g, float* __restrict__ disk,
                                                                        const int16_t* __restrict__ ncnt,
                                                                        int ox, int oy, int oz, uint32_t sweep,
@@ -1140,8 +1146,8 @@ __global__ __launch_bounds__(kWave * kSubWaves) void k_subsweep_full(DevGeom g, 
     const int total = (g.cps_x >> 1) * (g.cps_y >> 1) * ncz;
     const int t = (int)blockIdx.x * kSubWaves + wv;
     if (t >= total) return;
-    (void)subsweep_wave<NSLOT, NMC, 27 * NMC, OFF32, false, PB>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, full, full,
-                                                                 t, cz0);
+    (void)subsweep_wave<NSLOT, NMC, 27 * NMC, OFF32, false, PB, QK>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, full,
+                                                                     full, t, cz0);
 }
 
 
@@ -1344,7 +1350,7 @@ __device__ __forceinline__ void shift_store(float* p, float v) {
 // OFF32 (buffer < 4 GiB, PMC_SHIFT_OFF32=1): 32-bit byte offsets from the SGPR bases (global_load /
 // store with a VGPR offset), else 64-bit element addressing (default: the 32-bit form saves 170
 // address instructions and 27 VGPRs but not time, profiles/r04_shift_counters.json)
-template <int NSLOT, int U, int OFF32>
+template <int NSLOT, int U, int OFF32, bool S1 = false>
 __global__ __launch_bounds__(kShiftThreads) void k_shift(DevGeom g, const float* __restrict__ din,
                                                const int16_t* __restrict__ nin, float* __restrict__ dout,
                                                int16_t* __restrict__ nout, int f, float d,
@@ -1365,7 +1371,8 @@ __global__ __launch_bounds__(kShiftThreads) void k_shift(DevGeom g, const float*
     const int cps_f = f == 0 ? g.cps_x : (f == 1 ? g.cps_y : g.cps_z);
     const float Lf = f == 0 ? g.Lx : (f == 1 ? g.Ly : g.Lz);
     const int dir = (d <= 0) ? -1 : 1;                     // VS shiftCells.h:38-44
-    const float s = w * (float)dir;
+    // quirk S1 (pmc.h): the root copy's int s[3] (shiftCells.h:31,105) truncates w*dir
+    const float s = S1 ? (float)(int)(w * (float)dir) : w * (float)dir;
     const uint32_t plane = (uint32_t)g.cps_x * (uint32_t)g.cps_y;
     const int pp = p < nm ? p : 0;
     const int gsh = lane & ~(NSLOT - 1);
@@ -1478,7 +1485,7 @@ __global__ __launch_bounds__(kShiftThreads) void k_shift(DevGeom g, const float*
 // take rule is k_shift's (VS shiftCells.h:46-102) cell for cell, so the output is the same bits.
 // Lane groups: x fastest across a wave for f = 1, 2 (four neighbouring cells per wave load), runs
 // along x for f = 0.  Range: local planes [zl0, zl0 + nzr), halo planes included as in k_shift.
-template <int NSLOT, int R, int OFF32>
+template <int NSLOT, int R, int OFF32, bool S1 = false>
 __global__ __launch_bounds__(kShiftThreads) void k_shift_run(DevGeom g, const float* __restrict__ din,
                                                              const int16_t* __restrict__ nin, float* __restrict__ dout,
                                                              int16_t* __restrict__ nout, int f, float d,
@@ -1492,7 +1499,8 @@ __global__ __launch_bounds__(kShiftThreads) void k_shift_run(DevGeom g, const fl
     const int cps_f = f == 0 ? g.cps_x : (f == 1 ? g.cps_y : g.cps_z);
     const float Lf = f == 0 ? g.Lx : (f == 1 ? g.Ly : g.Lz);
     const int dir = (d <= 0) ? -1 : 1;                     // VS shiftCells.h:38-44
-    const float s = w * (float)dir;
+    // quirk S1 (pmc.h): the root copy's int s[3] (shiftCells.h:31,105) truncates w*dir
+    const float s = S1 ? (float)(int)(w * (float)dir) : w * (float)dir;
     const int len = f == 0 ? g.cps_x : (f == 1 ? g.cps_y : nzr);   // cells along f in the range
     const uint32_t nruns = (uint32_t)((len + R - 1) / R);
     // lane group -> (run a, the two other coordinates)
@@ -2756,6 +2764,8 @@ hipError_t launch_xfer(const XferCopy& cp, const XferFlags& w, uint64_t* ready, 
 // hipLaunchKernelGGL, or with dispatch-packet timing events when tm is given
 template <class K, class... A>
 static void launch_k(K kernel, dim3 grid, dim3 block, size_t lds, hipStream_t st, const LaunchTiming* tm, A... args) {
+    // the argument block is packed from these types: the host-only geometry must be sliced first
+    static_assert(!(std::is_same<A, HostGeom>::value || ...), "pass the DevGeom part of a HostGeom");
     if (tm && tm->start) hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)lds, st, tm->start, tm->stop, 0u, args...);
     else hipLaunchKernelGGL(kernel, grid, block, lds, st, args...);
 }
@@ -2862,6 +2872,42 @@ static void launch_direct_t(const DevGeom& g, float* disk, const int16_t* n, int
     }
 }
 
+// Quirks R1/R2 (pmc.h): every colour phase through the full-capacity one-cell-per-wave kernel,
+// instantiated with the quirk bits (the corrected-semantics kernels are not touched by them)
+template <int NSLOT, int NMC, bool OFF32, int QK>
+static void launch_quirk_t(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz, uint32_t sweep,
+                           unsigned long long* stats, int cz0, int ncz, hipStream_t st, const LaunchTiming* tm) {
+    const int64_t total = (int64_t)(g.cps_x / 2) * (g.cps_y / 2) * ncz;
+    const int full = 27 * g.nmax;
+    const size_t lds_full = sizeof(float) * (size_t)lds_floats_per_wave(full) * kSubWaves;
+    launch_k(k_subsweep_full<NSLOT, NMC, OFF32, 0, QK>, dim3((unsigned)((total + kSubWaves - 1) / kSubWaves)),
+             dim3(kWave * kSubWaves), lds_full, st, tm, g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz);
+}
+template <bool OFF32, int QK>
+static void launch_quirk_q(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz, uint32_t sweep,
+                           unsigned long long* stats, int cz0, int ncz, hipStream_t st, const LaunchTiming* tm) {
+    if (g.nmax == 16) launch_quirk_t<16, 16, OFF32, QK>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, st, tm);
+    else if (g.nmax == 32) launch_quirk_t<32, 32, OFF32, QK>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, st, tm);
+    else if (g.nslot == 8) launch_quirk_t<8, 0, OFF32, QK>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, st, tm);
+    else if (g.nslot == 16) launch_quirk_t<16, 0, OFF32, QK>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, st, tm);
+    else if (g.nslot == 32) launch_quirk_t<32, 0, OFF32, QK>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, st, tm);
+    else launch_quirk_t<64, 0, OFF32, QK>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, st, tm);
+}
+constexpr uint32_t kQuirksRng = PMC_FLAG_QUIRK_R1 | PMC_FLAG_QUIRK_R2;
+template <bool OFF32>
+static void launch_quirk_n(const HostGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz, uint32_t sweep,
+                           unsigned long long* stats, int cz0, int ncz, hipStream_t st, const LaunchTiming* tm) {
+    const DevGeom& kg = g;
+    switch (g.quirks & kQuirksRng) {
+        case PMC_FLAG_QUIRK_R1:
+            launch_quirk_q<OFF32, PMC_FLAG_QUIRK_R1>(kg, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, st, tm); break;
+        case PMC_FLAG_QUIRK_R2:
+            launch_quirk_q<OFF32, PMC_FLAG_QUIRK_R2>(kg, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, st, tm); break;
+        default:
+            launch_quirk_q<OFF32, kQuirksRng>(kg, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, st, tm); break;
+    }
+}
+
 template <bool OFF32>
 static void launch_direct_n(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz, uint32_t sweep,
                             unsigned long long* stats, int* ovf, int cz0, int ncz, float* mirror, int mode, hipStream_t st, const LaunchTiming* tm) {
@@ -2896,7 +2942,7 @@ static hipError_t skip_launch(hipStream_t st, const LaunchTiming* tm) {
     return hipSuccess;
 }
 
-hipError_t launch_subsweep_boundary(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
+hipError_t launch_subsweep_boundary(const HostGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
                                     uint32_t sweep, unsigned long long* stats, int* ovf, int zl_begin, int zl_end,
                                     float* mirror, int mirror_mode, hipStream_t st, const LaunchTiming* tm) {
     auto ceil_half = [](int v) { return v <= 0 ? 0 : (v + 1) / 2; };
@@ -2905,6 +2951,12 @@ hipError_t launch_subsweep_boundary(const DevGeom& g, float* disk, const int16_t
     if (cz1 > nczc) cz1 = nczc;
     if (cz1 <= cz0) return skip_launch(st, tm);
     const int64_t bytes = (int64_t)g.cps_x * g.cps_y * (g.nz_local + 2 * g.halo) * 3 * g.nmax * 4;
+    if (g.quirks & kQuirksRng) {   // (no mirror rows: pmc_slab_sweep turns the direct halo off with R1/R2)
+        if (mirror) return hipErrorInvalidValue;
+        if (bytes < ((int64_t)1 << 32)) launch_quirk_n<true>(g, disk, n, ox, oy, oz, sweep, stats, cz0, cz1 - cz0, st, tm);
+        else launch_quirk_n<false>(g, disk, n, ox, oy, oz, sweep, stats, cz0, cz1 - cz0, st, tm);
+        return hipGetLastError();
+    }
     if (bytes < ((int64_t)1 << 32)) launch_direct_n<true>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, cz1 - cz0, mirror, mirror_mode, st, tm);
     else launch_direct_n<false>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, cz1 - cz0, mirror, mirror_mode, st, tm);
     return hipGetLastError();
@@ -2952,7 +3004,7 @@ hipError_t launch_subsweep_planes2(const DevGeom& g, float* disk, const int16_t*
     return hipGetLastError();
 }
 
-hipError_t launch_subsweep_plane(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
+hipError_t launch_subsweep_plane(const HostGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
                                  uint32_t sweep, unsigned long long* stats, int* ovf, int zl, hipStream_t st,
                                  const LaunchTiming* tm) {
     // one colour plane z = zl (parity oz) of storage, halo planes included (-halo .. nz_local-1+halo):
@@ -2962,12 +3014,17 @@ hipError_t launch_subsweep_plane(const DevGeom& g, float* disk, const int16_t* n
     if (g.halo && (zl - 1 < -g.halo || zl + 1 > g.nz_local - 1 + g.halo)) return hipErrorInvalidValue;
     const int cz = (zl - oz) >> 1;   // arithmetic shift: floor, so zl = -1 (oz = 1) gives -1
     const int64_t bytes = (int64_t)g.cps_x * g.cps_y * (g.nz_local + 2 * g.halo) * 3 * g.nmax * 4;
+    if (g.quirks & kQuirksRng) {
+        if (bytes < ((int64_t)1 << 32)) launch_quirk_n<true>(g, disk, n, ox, oy, oz, sweep, stats, cz, 1, st, tm);
+        else launch_quirk_n<false>(g, disk, n, ox, oy, oz, sweep, stats, cz, 1, st, tm);
+        return hipGetLastError();
+    }
     if (bytes < ((int64_t)1 << 32)) launch_direct_n<true>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz, 1, nullptr, 0, st, tm);
     else launch_direct_n<false>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz, 1, nullptr, 0, st, tm);
     return hipGetLastError();
 }
 
-hipError_t launch_subsweep(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
+hipError_t launch_subsweep(const HostGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
                            uint32_t sweep, unsigned long long* stats, int* ovf, int zl_begin, int zl_end,
                            hipStream_t st, const LaunchTiming* tm) {
     // colour planes z = 2*cz + oz inside [zl_begin, zl_end)
@@ -2981,6 +3038,11 @@ hipError_t launch_subsweep(const DevGeom& g, float* disk, const int16_t* n, int 
     // (test hook: PMC_FORCE_ADDR64 takes the 64-bit path for any size)
     static const bool force64 = std::getenv("PMC_FORCE_ADDR64") != nullptr;
     const int64_t bytes = (int64_t)g.cps_x * g.cps_y * (g.nz_local + 2 * g.halo) * 3 * g.nmax * 4;
+    if (g.quirks & kQuirksRng) {
+        if (!force64 && bytes < ((int64_t)1 << 32)) launch_quirk_n<true>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, st, tm);
+        else launch_quirk_n<false>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, st, tm);
+        return hipGetLastError();
+    }
     if (!force64 && bytes < ((int64_t)1 << 32)) launch_subsweep_n<true>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st, tm);
     else launch_subsweep_n<false>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st, tm);
     return hipGetLastError();
@@ -2988,14 +3050,14 @@ hipError_t launch_subsweep(const DevGeom& g, float* disk, const int16_t* n, int 
 
 // Participants of k_sweep_small for a box (0: the box does not qualify -- nmax != 16, a slab, or
 // a colour phase over 4 cells per participant).  XCD 0 holds 512 waves of the 9.9 KB layout.
-int small_sweep_participants(const DevGeom& g) {
-    if (g.nmax != 16 || g.halo) return 0;
+int small_sweep_participants(const HostGeom& g) {
+    if (g.nmax != 16 || g.halo || g.quirks) return 0;   // (quirks: the eager path)
     const int64_t per_colour = (int64_t)(g.cps_x / 2) * (g.cps_y / 2) * (g.cps_z / 2);
     if (per_colour > 4 * 512) return 0;
     return per_colour < 512 ? (int)per_colour : 512;
 }
 
-hipError_t launch_sweep_small(const DevGeom& g, float* disk0, int16_t* n0, float* disk1, int16_t* n1, int cur,
+hipError_t launch_sweep_small(const HostGeom& g, float* disk0, int16_t* n0, float* disk1, int16_t* n1, int cur,
                               unsigned long long* stats, uint32_t* flags, unsigned* bar, uint64_t seed,
                               uint32_t first, int count, uint32_t plan_flags, hipStream_t st) {
     const int P = small_sweep_participants(g);
@@ -3020,7 +3082,8 @@ hipError_t launch_sweep_small(const DevGeom& g, float* disk0, int16_t* n0, float
         float* d1 = cur == 0 ? disk1 : disk0;
         int16_t* m0 = cur == 0 ? n0 : n1;
         int16_t* m1 = cur == 0 ? n1 : n0;
-        hipLaunchKernelGGL((k_sweep_small<16, 16, true>), dim3(8u * (unsigned)P), dim3(kWave), lds, st, g, d0, m0, d1,
+        const DevGeom& kg = g;
+        hipLaunchKernelGGL((k_sweep_small<16, 16, true>), dim3(8u * (unsigned)P), dim3(kWave), lds, st, kg, d0, m0, d1,
                            m1, stats, flags, bar, sp);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (sp.n & 1) cur ^= 1;
@@ -3029,12 +3092,12 @@ hipError_t launch_sweep_small(const DevGeom& g, float* disk0, int16_t* n0, float
     return hipSuccess;
 }
 
-hipError_t launch_shift(const DevGeom& g, const float* din, const int16_t* nin, float* dout,
+hipError_t launch_shift(const HostGeom& g, const float* din, const int16_t* nin, float* dout,
                         int16_t* nout, int f, float d, uint32_t* flags, hipStream_t st, const LaunchTiming* tm) {
     return launch_shift_planes(g, din, nin, dout, nout, f, d, flags, 0, g.nz_local, st, tm);
 }
 
-hipError_t launch_shift_planes(const DevGeom& g, const float* din, const int16_t* nin, float* dout,
+hipError_t launch_shift_planes(const HostGeom& g, const float* din, const int16_t* nin, float* dout,
                                int16_t* nout, int f, float d, uint32_t* flags, int zl_begin, int zl_end,
                                hipStream_t st, const LaunchTiming* tm) {
     if (zl_begin < -g.halo || zl_end > g.nz_local + g.halo || zl_end <= zl_begin) return hipErrorInvalidValue;
@@ -3066,22 +3129,29 @@ hipError_t launch_shift_planes(const DevGeom& g, const float* din, const int16_t
                          (f == 0 ? (int64_t)g.cps_y * nzr : (f == 1 ? (int64_t)g.cps_x * nzr : (int64_t)g.cps_x * g.cps_y));
     const int64_t lgs = kShiftThreads / g.nslot;
     const dim3 rgrid((unsigned)((runs + lgs - 1) / lgs));
-    auto go = [&](auto ns) {
+    const DevGeom& kg = g;   // the kernels' argument block
+    auto go = [&](auto ns, auto s1) {
         constexpr int NS = decltype(ns)::value;
+        constexpr bool S1 = decltype(s1)::value;
         if (run_env) {
-            if (off32) launch_k(k_shift_run<NS, kShiftRun, 1>, rgrid, block, 0, st, tm, g, din, nin, dout, nout, f, d, flags, z0, nzr);
-            else launch_k(k_shift_run<NS, kShiftRun, 0>, rgrid, block, 0, st, tm, g, din, nin, dout, nout, f, d, flags, z0, nzr);
+            if (off32) launch_k(k_shift_run<NS, kShiftRun, 1, S1>, rgrid, block, 0, st, tm, kg, din, nin, dout, nout, f, d, flags, z0, nzr);
+            else launch_k(k_shift_run<NS, kShiftRun, 0, S1>, rgrid, block, 0, st, tm, kg, din, nin, dout, nout, f, d, flags, z0, nzr);
             return;
         }
-        if (off32) launch_k(k_shift<NS, U, 1>, grid, block, 0, st, tm, g, din, nin, dout, nout, f, d, flags, z0);
-        else launch_k(k_shift<NS, U, 0>, grid, block, 0, st, tm, g, din, nin, dout, nout, f, d, flags, z0);
+        if (off32) launch_k(k_shift<NS, U, 1, S1>, grid, block, 0, st, tm, kg, din, nin, dout, nout, f, d, flags, z0);
+        else launch_k(k_shift<NS, U, 0, S1>, grid, block, 0, st, tm, kg, din, nin, dout, nout, f, d, flags, z0);
     };
-    switch (g.nslot) {
-        case 8: go(std::integral_constant<int, 8>{}); break;
-        case 16: go(std::integral_constant<int, 16>{}); break;
-        case 32: go(std::integral_constant<int, 32>{}); break;
-        default: go(std::integral_constant<int, 64>{}); break;
-    }
+    // quirk S1 (pmc.h): the integer offset -- its own instantiations, the default kernels unchanged
+    auto by_slot = [&](auto s1) {
+        switch (g.nslot) {
+            case 8: go(std::integral_constant<int, 8>{}, s1); break;
+            case 16: go(std::integral_constant<int, 16>{}, s1); break;
+            case 32: go(std::integral_constant<int, 32>{}, s1); break;
+            default: go(std::integral_constant<int, 64>{}, s1); break;
+        }
+    };
+    if (g.quirks & PMC_FLAG_QUIRK_S1) by_slot(std::true_type{});
+    else by_slot(std::false_type{});
     return hipGetLastError();
 }
 

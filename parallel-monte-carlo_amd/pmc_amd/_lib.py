@@ -46,6 +46,7 @@ class Result(C.Structure):
 
 
 PMC_FLAG_FULL_SHUFFLE = 1
+PMC_FLAG_QUIRK_R1, PMC_FLAG_QUIRK_R2, PMC_FLAG_QUIRK_S1 = 2, 4, 8     # reference quirks (include/pmc.h)
 PMC_OK, PMC_ERR_ARG, PMC_ERR_HIP, PMC_ERR_OVERFLOW, PMC_ERR_RANGE, PMC_ERR_NODEV = 0, -1, -2, -3, -4, -5
 PMC_IPC_HANDLE_BYTES = 1024     # include/pmc.h
 PMC_LAYOUT_REFERENCE, PMC_LAYOUT_PACKED = 0, 1

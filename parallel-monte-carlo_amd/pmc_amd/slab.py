@@ -129,7 +129,7 @@ class SlabDriver:
         self.stream = stream
         if not halo:
             halo = int(os.environ.get("PMC_SLAB_HALO", "1") or 1)
-        if flags & 1:            # PMC_FLAG_FULL_SHUFFLE: up to 8 runs a sweep, one-plane halos
+        if flags & 7:            # FULL_SHUFFLE (up to 8 runs a sweep) or quirks R1/R2: one-plane halos
             halo = 1
         self.halo = halo
         self.ctx = PmcContext(cps, cps_y=cps_y, cps_z=self.g.cps_z, nz_local=nz_local, z0=self.g.z0, halo=halo,
