@@ -495,9 +495,12 @@ def main() -> int:
                     help="sweeps run on the timed start state right before the timed region, which is "
                          "then restored on the device (the GPU comes out of the host analysis idle "
                          "and needs ~10 sweeps to reach its steady clock; 0: off)")
-    ap.add_argument("--timing-every", type=int, default=4,
+    ap.add_argument("--timing-every", type=int, default=0,
                     help="per-launch HIP events on the launches of every k-th timed sweep (the roofline's "
-                         "kernel times; events on every launch cost ~1.3%% of the sweep)")
+                         "kernel times).  Default: 4 for a whole box (events on every launch cost ~1.3%% of "
+                         "its sweep); ceil(steps/2) (>= 4) for the slab driver, whose 0.38 ms sweep at 8 "
+                         "ranks is host-issue-bound while events ride on its launches (a timed sweep "
+                         "+55 us; every 4th: +3.5%%, every 20th: +0.3%%, profiles/r06s_event_every_ab.txt)")
     ap.add_argument("--slab", action="store_true", help="config 3 through the z-slab driver with one rank")
     ap.add_argument("--self-rccl", action="store_true",
                     help="one slab rank: halos through a one-rank RCCL communicator (default for config 5)")
@@ -706,15 +709,17 @@ def main() -> int:
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     first = args.warmup
+    t_issue = None
     if args.graph and not slab:
         sim.run_graph(first, args.steps)
     else:
         timed = not args.no_events
-        every = max(1, args.timing_every)
+        every = args.timing_every if args.timing_every > 0 else (max(4, -(-args.steps // 2)) if slab else 4)
         for k in range(args.steps):
             if timed and every > 1:
                 sim.timing_pause(k % every != 0)   # events on sweeps 0, every, 2*every, ...
             one_sweep(first + k)
+        t_issue = time.perf_counter() - t0     # host time to issue the K steps (the GPU may still run)
         finish()
     torch.cuda.synchronize()
     barrier()
@@ -889,6 +894,9 @@ def main() -> int:
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
+            # host time spent issuing a step's launches (pmc_sweep / pmc_slab_sweep calls, no waits):
+            # close to ms_per_step means the host, not the GPU, sets the pace
+            "host_issue_ms_per_step": (t_issue / args.steps * 1e3) if t_issue is not None else None,
             **({"step": "one colour phase"} if config == "2" else {}),
             "higher_is_better": True,
             # configs 3 -> 4 are one fixed box over 1..N GPUs (strong); config 5 fixes the work per GPU

@@ -14,8 +14,8 @@
 #   slab1            config 3 through the slab driver, one rank, local halos
 #   bench5box        the whole 256^3 / 8e7 box on one GPU
 #   bench5           config 5 rehearsal (one 256x256x32 slab, halos through a one-rank RCCL communicator)
-#   emu<R>[-<tp>][-d<us>]   config-4 rehearsal of R ranks (one rank's slab), transport tp (local|ipc|rccl,
-#                    default local), injected exchange delay us
+#   emu<R>[-<tp>][-d<us>][-ne|-t<k>]   config-4 rehearsal of R ranks (one rank's slab), transport tp (local|ipc|rccl,
+#                    default local), injected exchange delay us, no events / events every k-th sweep
 #   mp2bench         bench.py --gpus 2 --same-device --config 4 (rank processes, IPC); mp4bench, mp8bench: 4, 8
 #   rocprof          rocprofv3 --kernel-trace --stats of the default bench command
 #   trace8[d<us>]    rocprofv3 kernel trace of the 8-rank IPC rehearsal (injected exchange delay us) +
@@ -36,8 +36,9 @@ import json, sys
 for ln in open(sys.argv[1]):
     if ln.startswith("{"):
         d = json.loads(ln); r = d.get("roofline") or {}; p = d.get("parity") or {}
-        print("%s value %.4g ms/step %.4f launch %s phase %s shift %s frac %s parity %s/%s" % (
+        print("%s value %.4g ms/step %.4f issue %s launch %s phase %s shift %s frac %s parity %s/%s" % (
             sys.argv[1].split("/")[-1], d["value"], d["ms_per_step"],
+            "%.4f" % d["host_issue_ms_per_step"] if d.get("host_issue_ms_per_step") else None,
             "%.4f" % r["launch_ms"] if r.get("launch_ms") else None,
             "%.4f" % r["phase_ms"] if r.get("phase_ms") else None,
             "%.4f" % r["shift_ms"] if r.get("shift_ms") else None,
@@ -70,13 +71,13 @@ for spec in "$@"; do
         bench5) timeout -k 10 300 python bench.py --config 5 --no-cpu-baseline --steps 20 --warmup 5 > $log 2>&1 ;;
         bench5box) timeout -k 10 400 python bench.py --config 5box --no-cpu-baseline --steps 10 --warmup 3 > $log 2>&1 ;;
         emu*)
-            spec=${step#emu}; R=${spec%%-*}; tp=local; dl=0
+            spec=${step#emu}; R=${spec%%-*}; tp=local; dl=0; extra=
             IFS=- read -ra parts <<< "$spec"
             for p in "${parts[@]:1}"; do
-                case $p in d*) dl=${p#d} ;; *) tp=$p ;; esac
+                case $p in d*) dl=${p#d} ;; ne) extra=--no-events ;; t*) extra="--timing-every ${p#t}" ;; *) tp=$p ;; esac
             done
             timeout -k 10 300 python bench.py --config 4 --emulate-ranks $R --transport $tp --xfer-delay-us $dl \
-                --no-cpu-baseline --steps 100 --warmup 20 > $log 2>&1 ;;
+                --no-cpu-baseline --steps 100 --warmup 20 $extra > $log 2>&1 ;;
         mp2bench) timeout -k 10 400 python bench.py --gpus 2 --same-device --config 4 --steps 20 --warmup 5 \
                 --rank-timeout 360 > $log 2>&1 ;;
         mp4bench|mp8bench) R=${step:2:1}; timeout -k 10 500 python bench.py --gpus $R --same-device --config 4 --steps 10 \
