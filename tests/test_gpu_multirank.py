@@ -316,6 +316,14 @@ def _world_vs_oracle(pmc, oracle, world, cps, nz, atoms, first, count, lattice_c
 
 
 @pytest.mark.timeout(400)
+def test_slab_long_run_world4_64_equals_oracle(pmc, oracle):
+    """4 slab ranks of the 64^3 / 1e6 box over 24 sweeps from the lattice start (the counts spread
+    from 4-5 per cell through the relaxation; every exchange kind recurs many times): bitwise equal
+    to the oracle's whole-box run."""
+    _world_vs_oracle(pmc, oracle, 4, 64, 16, 1_000_000, 0, 24)
+
+
+@pytest.mark.timeout(400)
 def test_config4_world8_128_equals_oracle(pmc, oracle):
     """BASELINE config 4 at its workload: the 128^3-cell, 1e7-particle box in 8 z-slabs of 16
     planes (pmc_init_lattice_global: every rank starts from its planes of the one-GPU lattice),

@@ -318,6 +318,27 @@ def test_single_colour_parity_64(pmc, oracle):
     assert ctx.stats() == st.stats.as_dict()
 
 
+def test_long_run_parity_64(pmc, oracle):
+    """BASELINE config 2's box (64^3 cells, 1e6 particles) over 30 full sweeps from the lattice start,
+    through the relaxation where the cell counts spread (the lattice's 4-5 per cell becomes 0-13): every
+    occupied slot, the counts, the four counters and the energy equal the oracle's bit for bit at
+    sweeps 10 and 30.  Tolerance: none."""
+    oracle.set_threads(16)
+    ctx = _ctx(pmc, 64)
+    ctx.init_lattice(1_000_000)
+    st = _ostate(oracle, 64)
+    st.init_lattice(1_000_000)
+    for first, count in ((0, 10), (10, 20)):
+        r = ctx.start(first, count)
+        assert st.run(first, count) == 0
+        _assert_same(oracle, ctx, st, 16)
+        assert ctx.stats() == st.stats.as_dict()
+        assert r["e_final"] == st.energy()
+        assert ctx.error_flags() == 0
+    _, n = ctx.copy_out()
+    assert n.max() > 8      # the counts did spread: the staging's overflow passes (slots >= 8) ran
+
+
 def test_full_sweeps_parity_128(pmc, oracle):
     """BASELINE config 3 (128^3 cells, 1e7 particles): two full sweeps -- all 8 colour phases and
     shiftCells, one shift along z -- compared with the oracle bit for bit (every occupied slot,
