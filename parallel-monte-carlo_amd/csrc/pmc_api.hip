@@ -308,7 +308,7 @@ int enqueue_sweep(pmc_ctx* c, uint32_t sweep, bool chains = true) {
         pmc_colour_offset(plan.order[k], o);
         LaunchTiming lt;
         hipError_t e = launch_subsweep(c->G, c->disk[c->cur], c->n[c->cur], o[0], o[1], o[2], sweep,
-                                       c->stats, c->ovf, 0, c->P.nz_local, c->stream, next_timing(c, 0, &lt));
+                                       c->stats, c->ovf, 0, c->P.nz_local, c->stream, next_timing(c, 0, &lt), true);
         if (e != hipSuccess) return hip_fail(e, "subsweep launch");
     }
     LaunchTiming lt;
@@ -530,7 +530,7 @@ int pmc_subsweep_range(pmc_ctx* c, float* d_disk, const int16_t* d_n, const int 
     }
     LaunchTiming lt;
     hipError_t e = launch_subsweep(c->G, run, d_n, offset[0], offset[1], offset[2], sweep, c->stats, c->ovf,
-                                   zl_begin, zl_end, c->stream, next_timing(c, 0, &lt));
+                                   zl_begin, zl_end, c->stream, next_timing(c, 0, &lt), !c->slab);
     if (e == hipSuccess && conv) e = launch_relayout(c->conv[0], d_disk, c->cells, c->P.nmax, 0, c->stream);
     return e == hipSuccess ? PMC_OK : hip_fail(e, "subsweep launch");
 }

@@ -105,9 +105,10 @@ struct LaunchTiming {
 // Launchers (pmc_kernels.hip).  All asynchronous on `st`.
 // ovf: int[1 + cells_per_colour] scratch (overflow queue for the full-capacity fallback)
 // only cells in local planes [zl_begin, zl_end) of the colour are visited
+// solo: the launch has the GPU to itself (no concurrent chain): a short one ends in single-cell waves
 hipError_t launch_subsweep(const HostGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
                            uint32_t sweep, unsigned long long* stats, int* ovf, int zl_begin, int zl_end,
-                           hipStream_t st, const LaunchTiming* tm = nullptr);
+                           hipStream_t st, const LaunchTiming* tm = nullptr, bool solo = false);
 // the slab driver's boundary planes: full LDS capacity (no overflow queue), every written-back row
 // also stored to `mirror` (mirror_mode 0: packed colour rows ta + tb*cps_x/2, 1: plane rows;
 // mirror may be null)

@@ -856,7 +856,7 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
                                               uint32_t sweep, unsigned long long* __restrict__ stats,
                                               float* __restrict__ px_, int lcap_rt, int cap, int t,
                                               int cz0, float* __restrict__ mirror = nullptr,
-                                              int mirror_mode = 0, int czs = 1) {
+                                              int mirror_mode = 0, int czs = 1, int zlog = 0, int ncz_z = 0) {
     const int lane = threadIdx.x & (kWave - 1);
     const int nm = NMC > 0 ? NMC : g.nmax;
     const int lcap = LCAP > 0 ? LCAP : lcap_rt;
@@ -865,7 +865,7 @@ __device__ __forceinline__ bool subsweep_wave(const DevGeom& g, float* __restric
     float* py_ = px_ + stride;
     float* pz_ = py_ + stride;
     float* buf = pz_ + stride;
-    const CellGeo cg = cell_geo(g, t, cz0, ox, oy, oz, 0, 0, czs);
+    const CellGeo cg = cell_geo(g, t, cz0, ox, oy, oz, zlog, ncz_z, czs);
     // quirk R2 (pmc.h): curand_init(1234, id, 0) on every launch -- the sweep index leaves the counters
     if (QK & PMC_FLAG_QUIRK_R2) sweep = 0u;
     PMC_STAMP(0);
@@ -1027,6 +1027,39 @@ __global__ __launch_bounds__(kWave * kSubWaves) __attribute__((amdgpu_waves_per_
         if ((threadIdx.x & (kWave - 1)) == 0) ovf[kOvfHead + atomicAdd(&ovf[kOvfCount], 1)] = t;
     }
 #endif
+}
+
+// Mixed main launch (PMC_MIXED_SINGLES=<s>, A/B switch): each XCD's contiguous run of cells is
+// visited two cells per wave, except its last s cells, one per wave.  The hardware dispatches blocks
+// in order, so the single-cell waves are the launch's last: the tail a launch spends draining its
+// last round of wave slots is then half a two-cell wave lifetime.  Same cells, same visit: results
+// bit-identical.  Grid: 8 * (pair_waves + singles) one-wave blocks (block b on XCD b % 8).
+template <int NSLOT, int NMC, bool OFF32>
+__global__ __launch_bounds__(kWave * kSubWaves) __attribute__((amdgpu_waves_per_eu(PMC_MAIN_WAVES, PMC_MAIN_WAVES))) void k_subsweep_mixed(
+    DevGeom g, float* __restrict__ disk, const int16_t* __restrict__ ncnt, int ox, int oy, int oz, uint32_t sweep,
+    unsigned long long* __restrict__ stats, int cap, int* __restrict__ ovf, int cz0, int ncz, int per_xcd, int pair_waves) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* px_ = smem;
+    const int b = (int)blockIdx.x;
+    const int base = (b & 7) * per_xcd;
+    const int r = b >> 3;
+    const int total = (g.cps_x >> 1) * (g.cps_y >> 1) * ncz;
+    const int end = base + per_xcd < total ? base + per_xcd : total;
+    const int zlog = (PMC_ZGROUP <= 4 || (ncz & ((1 << kZGroupLog) - 1)) == 0) ? kZGroupLog : 0;
+    if (r < pair_waves) {
+        const int p = base + 2 * r;
+        if (p >= end) return;
+        subsweep_pair<NSLOT, NMC, kMainCap, OFF32>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, kMainCap, cap, p, p + 1,
+                                                   p + 1 < end, cz0, zlog, ncz, ovf);
+    } else {
+        const int p = base + 2 * pair_waves + (r - pair_waves);
+        if (p >= end) return;
+        if (!subsweep_wave<NSLOT, NMC, kMainCap, OFF32>(g, disk, ncnt, ox, oy, oz, sweep, stats, px_, kMainCap, cap, p,
+                                                        cz0, nullptr, 0, 1, zlog, ncz)) {
+            if ((threadIdx.x & (kWave - 1)) == 0)
+                ovf[kOvfHead + atomicAdd(&ovf[kOvfCount], 1)] = cell_geo(g, p, cz0, ox, oy, oz, zlog, ncz).t;
+        }
+    }
 }
 
 // Boundary-plane launch of the slab driver: ONE cell per wave at the main launch's capacity (5 KiB
@@ -2806,7 +2839,7 @@ static void launch_direct_t(const DevGeom& g, float* disk, const int16_t* n, int
 template <int NSLOT, int NMC, bool OFF32>
 static void launch_subsweep_t(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
                               uint32_t sweep, unsigned long long* stats, int* ovf, int cz0, int ncz,
-                              hipStream_t st, const LaunchTiming* tm) {
+                              hipStream_t st, const LaunchTiming* tm, bool solo) {
     const int64_t total = (int64_t)(g.cps_x / 2) * (g.cps_y / 2) * ncz;
     const int64_t waves = (total + PMC_CELLS_PER_WAVE - 1) / PMC_CELLS_PER_WAVE;
     const int64_t blocks = (waves + kSubWaves - 1) / kSubWaves;
@@ -2828,6 +2861,22 @@ static void launch_subsweep_t(const DevGeom& g, float* disk, const int16_t* n, i
         return;
     }
     size_t lds = sizeof(float) * (size_t)lds_floats_per_wave(kMainCap) * kSubWaves;
+    // Solo launches (nothing else on the GPU) of at most two rounds of the chip's wave slots (<= 32768
+    // cells: 16384 two-cell waves) end in single-cell waves, 1/8 of each XCD's cells
+    // (k_subsweep_mixed): config 2's phase -3.7% (profiles/r06m_mixed_tail_ab.txt).  Launches beside
+    // another chain drain their tails under its work (4-rank rehearsal +1.9% with them) and keep
+    // k_subsweep.  PMC_MIXED_SINGLES=<n> forces n
+    // single-cell waves per XCD on every launch, 0 turns it off (A/B switch).
+    static const int64_t mixed_env = env_cells("PMC_MIXED_SINGLES", -1);
+    const int64_t mixed = mixed_env >= 0 ? mixed_env : ((solo && total <= 32768) ? (total + 63) / 64 : 0);
+    if (mixed > 0 && kSubWaves == 1 && PMC_CELLS_PER_WAVE == 2) {
+        const int per_xcd = (int)((total + 7) / 8);
+        const int singles = (int)(mixed < per_xcd ? mixed : per_xcd);
+        const int pair_waves = (per_xcd - singles) / 2;
+        const int waves_xcd = pair_waves + (per_xcd - 2 * pair_waves);
+        launch_k(k_subsweep_mixed<NSLOT, NMC, OFF32>, dim3(8u * (unsigned)waves_xcd), dim3(kWave), lds, st, tm, g, disk,
+                 n, ox, oy, oz, sweep, stats, cap, ovf, cz0, ncz, per_xcd, pair_waves);
+    } else
     launch_k(k_subsweep<NSLOT, NMC, OFF32>, dim3((unsigned)blocks), dim3(kWave * kSubWaves), lds, st, tm, g, disk, n,
              ox, oy, oz, sweep, stats, cap, ovf, cz0, ncz);
     if (cap < full) {
@@ -2922,13 +2971,13 @@ static void launch_direct_n(const DevGeom& g, float* disk, const int16_t* n, int
 template <bool OFF32>
 static void launch_subsweep_n(const DevGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
                               uint32_t sweep, unsigned long long* stats, int* ovf, int cz0, int ncz,
-                              hipStream_t st, const LaunchTiming* tm) {
-    if (g.nmax == 16) launch_subsweep_t<16, 16, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st, tm);
-    else if (g.nmax == 32) launch_subsweep_t<32, 32, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st, tm);
-    else if (g.nslot == 8) launch_subsweep_t<8, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st, tm);
-    else if (g.nslot == 16) launch_subsweep_t<16, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st, tm);
-    else if (g.nslot == 32) launch_subsweep_t<32, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st, tm);
-    else launch_subsweep_t<64, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st, tm);
+                              hipStream_t st, const LaunchTiming* tm, bool solo) {
+    if (g.nmax == 16) launch_subsweep_t<16, 16, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st, tm, solo);
+    else if (g.nmax == 32) launch_subsweep_t<32, 32, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st, tm, solo);
+    else if (g.nslot == 8) launch_subsweep_t<8, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st, tm, solo);
+    else if (g.nslot == 16) launch_subsweep_t<16, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st, tm, solo);
+    else if (g.nslot == 32) launch_subsweep_t<32, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st, tm, solo);
+    else launch_subsweep_t<64, 0, OFF32>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st, tm, solo);
 }
 
 // a timed launch with nothing to visit (a chain whose planes hold no plane of the colour): its
@@ -3026,7 +3075,7 @@ hipError_t launch_subsweep_plane(const HostGeom& g, float* disk, const int16_t* 
 
 hipError_t launch_subsweep(const HostGeom& g, float* disk, const int16_t* n, int ox, int oy, int oz,
                            uint32_t sweep, unsigned long long* stats, int* ovf, int zl_begin, int zl_end,
-                           hipStream_t st, const LaunchTiming* tm) {
+                           hipStream_t st, const LaunchTiming* tm, bool solo) {
     // colour planes z = 2*cz + oz inside [zl_begin, zl_end)
     auto ceil_half = [](int v) { return v <= 0 ? 0 : (v + 1) / 2; };
     const int nczc = g.nz_local / 2;
@@ -3043,8 +3092,8 @@ hipError_t launch_subsweep(const HostGeom& g, float* disk, const int16_t* n, int
         else launch_quirk_n<false>(g, disk, n, ox, oy, oz, sweep, stats, cz0, ncz, st, tm);
         return hipGetLastError();
     }
-    if (!force64 && bytes < ((int64_t)1 << 32)) launch_subsweep_n<true>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st, tm);
-    else launch_subsweep_n<false>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st, tm);
+    if (!force64 && bytes < ((int64_t)1 << 32)) launch_subsweep_n<true>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st, tm, solo);
+    else launch_subsweep_n<false>(g, disk, n, ox, oy, oz, sweep, stats, ovf, cz0, ncz, st, tm, solo);
     return hipGetLastError();
 }
 

@@ -318,6 +318,22 @@ def test_single_colour_parity_64(pmc, oracle):
     assert ctx.stats() == st.stats.as_dict()
 
 
+def test_graph_sweeps_parity_64(pmc, oracle):
+    """Sweeps replayed as one hipGraph of single-chain launches on the 64^3 / 1e6 box: each colour
+    phase is one solo launch of 32768 cells, which ends in single-cell waves (k_subsweep_mixed).
+    Bitwise equal to the oracle over 3 sweeps."""
+    oracle.set_threads(16)
+    ctx = _ctx(pmc, 64)
+    ctx.init_lattice(1_000_000)
+    ctx.run_graph(5, 3)
+    st = _ostate(oracle, 64)
+    st.init_lattice(1_000_000)
+    assert st.run(5, 3) == 0
+    _assert_same(oracle, ctx, st, 16)
+    assert ctx.stats() == st.stats.as_dict()
+    assert ctx.error_flags() == 0
+
+
 def test_long_run_parity_64(pmc, oracle):
     """BASELINE config 2's box (64^3 cells, 1e6 particles) over 30 full sweeps from the lattice start,
     through the relaxation where the cell counts spread (the lattice's 4-5 per cell becomes 0-13): every
@@ -393,14 +409,18 @@ def test_single_colour_parity_128(pmc, oracle):
 @pytest.mark.parametrize("env,nmax", [({"PMC_SUBSWEEP_CAP": "64", "PMC_SMALL_LAUNCH": "0"}, 32),
                                       ({"PMC_FORCE_ADDR64": "1"}, 16),
                                       ({"PMC_FORCE_ADDR64": "1", "PMC_SUBSWEEP_CAP": "64", "PMC_SMALL_LAUNCH": "0"}, 16),
-                                      ({"PMC_SMALL_LAUNCH": "0"}, 16)])
+                                      ({"PMC_SMALL_LAUNCH": "0"}, 16),
+                                      ({"PMC_MIXED_SINGLES": "5", "PMC_SMALL_LAUNCH": "0"}, 16),
+                                      ({"PMC_MIXED_SINGLES": "5", "PMC_SMALL_LAUNCH": "0", "PMC_SUBSWEEP_CAP": "64"}, 16)])
 def test_fallback_and_addr64_paths(oracle, env, nmax):
     """Test hooks for launch variants the default configs never take, each bit-identical to the
     oracle: PMC_SUBSWEEP_CAP forces a tiny LDS capacity, so (almost) every cell goes to the
     full-capacity fallback launch; PMC_FORCE_ADDR64 forces the 64-bit disk addressing used for
     buffers of 4 GiB and more; PMC_SMALL_LAUNCH=0 takes this 8^3 box through the main two-cell
     launch + fallback instead of the one-launch full-capacity path small boxes default to.  Runs in
-    a subprocess (the hooks are read once)."""
+    a subprocess (the hooks are read once).  PMC_MIXED_SINGLES=5 ends every launch's XCD runs in
+    single-cell waves (k_subsweep_mixed, the default for solo launches of <= 32768 cells), with and
+    without forced overflow of those single-cell waves."""
     import os
     import subprocess
     import sys

@@ -10,7 +10,7 @@
 #   file:<path>      one GPU test file
 #   smoke            __graft_entry__.smoke()
 #   bench            default bench line (config 3, the driver's --steps 20 --warmup 5)
-#   bench2           config 2 (pmc_phase_seq blocks); bench2pc: one pmc_phase call per step
+#   bench2           config 2 (one pmc_phase call per step)
 #   slab1            config 3 through the slab driver, one rank, local halos
 #   bench5box        the whole 256^3 / 8e7 box on one GPU
 #   bench5           config 5 rehearsal (one 256x256x32 slab, halos through a one-rank RCCL communicator)
@@ -66,7 +66,6 @@ for spec in "$@"; do
         smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $log 2>&1 ;;
         bench) timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $log 2>&1 ;;
         bench2) timeout -k 10 300 python bench.py --config 2 --steps 160 --warmup 8 > $log 2>&1 ;;
-        bench2pc) timeout -k 10 300 python bench.py --config 2 --steps 160 --warmup 8 --phase-calls > $log 2>&1 ;;
         slab1) timeout -k 10 300 python bench.py --slab --no-cpu-baseline --steps 20 --warmup 5 > $log 2>&1 ;;
         bench5) timeout -k 10 300 python bench.py --config 5 --no-cpu-baseline --steps 20 --warmup 5 > $log 2>&1 ;;
         bench5box) timeout -k 10 400 python bench.py --config 5box --no-cpu-baseline --steps 10 --warmup 3 > $log 2>&1 ;;
